@@ -1,0 +1,749 @@
+// shmem_reduce.cpp -- C-ABI layer of libosgpu_reduce.so.
+//
+// Replaces the reduce-to-all entry points of the reference
+// (SHMEM_REDUCE_TYPE_OP, src/reductions.c:139-154, instantiated at :248-297)
+// with the same 44 signatures.  Where the reference walks its peers with a
+// blocking 64-element shmem_getmem per chunk and folds through a function
+// pointer per element (udr_<T>_to_all, src/reductions.c:32-120), this layer
+// picks one of three MI355X paths:
+//
+//   P2P   (device-resident, every active PE's device heap addressable here):
+//         the reference's pull schedule as ONE combine kernel that streams
+//         all PE_size sources -- local HBM or peer HBM over xGMI -- in the
+//         reference's fold order (bit-exact, including floating point);
+//   RCCL  (device-resident, one process per GPU with an RCCL communicator):
+//         ncclAllReduce over xGMI stands in for the barrier + pull schedule;
+//   HOST  (host symmetric-heap arguments): peers' sources staged through the
+//         runtime's shmem_getmem (UCX) into pinned buffers, H2D, the same
+//         combine kernel, D2H.
+//
+// The two shmem_barrier calls of the reference (:82, :113) keep their roles
+// on the P2P and HOST paths (sources ready / peers done reading).
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "../../include/osgpu_reduce.h"
+#include "combine.hpp"
+
+namespace {
+
+// ------------------------------------------------------------------ errors
+
+thread_local char g_err[512];
+
+void set_err(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+// The shmem_* entry points are void (src/reductions.c:139-154); the
+// reference logs LOG_FATAL and returns on OOM (:55-61) and asserts on
+// transport errors (src/shmemc/comms.c:250).  Silent wrong results are
+// worse than both, so an unrecoverable error is reported and aborts.
+[[noreturn]] void fatal(const char *where, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "osgpu_reduce: %s: %s\n", where, buf);
+    fflush(stderr);
+    abort();
+}
+
+#define HIPCHK(where, call)                                                    \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) fatal(where, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+// --------------------------------------------------------------- type info
+
+size_t type_size(int t)
+{
+    switch (t) {
+    case OSGPU_T_SHORT: return sizeof(short);
+    case OSGPU_T_INT: return sizeof(int);
+    case OSGPU_T_LONG: return sizeof(long);
+    case OSGPU_T_LONGLONG: return sizeof(long long);
+    case OSGPU_T_FLOAT: return sizeof(float);
+    case OSGPU_T_DOUBLE: return sizeof(double);
+    case OSGPU_T_LONGDOUBLE: return sizeof(long double);
+    case OSGPU_T_COMPLEXF: return 2 * sizeof(float);
+    case OSGPU_T_COMPLEXD: return 2 * sizeof(double);
+    }
+    return 0;
+}
+
+bool has_op(int t, int op)
+{
+    if (t < OSGPU_T_SHORT || t > OSGPU_T_COMPLEXD) return false;
+    switch (op) {
+    case OSGPU_OP_SUM: case OSGPU_OP_PROD: return true;
+    case OSGPU_OP_AND: case OSGPU_OP_OR: case OSGPU_OP_XOR: return t <= OSGPU_T_LONGLONG;
+    case OSGPU_OP_MAX: case OSGPU_OP_MIN: return t <= OSGPU_T_LONGDOUBLE;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------- PE services
+
+struct PeOps {
+    int (*my_pe)(void) = nullptr;
+    int (*n_pes)(void) = nullptr;
+    void (*barrier)(int, int, int, long *) = nullptr;
+    void (*getmem)(void *, const void *, size_t, int) = nullptr;
+};
+
+std::mutex g_mu;
+PeOps g_ops;
+bool g_ops_set = false;
+
+PeOps pe_ops()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ops_set) {
+        // bind to the OpenSHMEM runtime the application links (the reference
+        // library exports these as strong or weak symbols)
+        g_ops.my_pe = (int (*)(void)) dlsym(RTLD_DEFAULT, "shmem_my_pe");
+        g_ops.n_pes = (int (*)(void)) dlsym(RTLD_DEFAULT, "shmem_n_pes");
+        g_ops.barrier = (void (*)(int, int, int, long *)) dlsym(RTLD_DEFAULT, "shmem_barrier");
+        g_ops.getmem = (void (*)(void *, const void *, size_t, int)) dlsym(RTLD_DEFAULT,
+                                                                          "shmem_getmem");
+        g_ops_set = true;
+    }
+    return g_ops;
+}
+
+// -------------------------------------------------------- device sym. heap
+
+struct HeapEntry {
+    char *base = nullptr;
+    size_t bytes = 0;
+};
+std::vector<HeapEntry> g_heap;  // indexed by PE
+
+bool heap_lookup(int pe, HeapEntry *out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (pe < 0 || (size_t) pe >= g_heap.size() || !g_heap[pe].base) return false;
+    *out = g_heap[pe];
+    return true;
+}
+
+// ---------------------------------------------------------------- RCCL
+
+struct Rccl {
+    ncclComm_t world = nullptr;
+    int npes = 0, me = -1;
+} g_rccl;
+
+int g_path = -1;  // -1: not yet read from the environment
+
+int path_mode()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_path < 0) {
+        g_path = OSGPU_PATH_AUTO;
+        const char *e = getenv("OSGPU_REDUCE_PATH");
+        if (e && !strcmp(e, "p2p")) g_path = OSGPU_PATH_P2P;
+        if (e && !strcmp(e, "rccl")) g_path = OSGPU_PATH_RCCL;
+    }
+    return g_path;
+}
+
+// -------------------------------------------------------- per-thread state
+
+struct ThreadCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    bool user_stream = false;
+    void *dscratch = nullptr;
+    size_t dscratch_bytes = 0;
+    void *hstage = nullptr;  // pinned
+    size_t hstage_bytes = 0;
+};
+thread_local ThreadCtx t_ctx;
+
+hipStream_t thread_stream(const char *where)
+{
+    int dev = 0;
+    HIPCHK(where, hipGetDevice(&dev));
+    if (t_ctx.stream && (t_ctx.user_stream || t_ctx.device == dev)) return t_ctx.stream;
+    HIPCHK(where, hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
+    t_ctx.device = dev;
+    t_ctx.user_stream = false;
+    return t_ctx.stream;
+}
+
+void *device_scratch(const char *where, size_t bytes)
+{
+    if (t_ctx.dscratch_bytes < bytes) {
+        if (t_ctx.dscratch) HIPCHK(where, hipFree(t_ctx.dscratch));
+        t_ctx.dscratch = nullptr;
+        t_ctx.dscratch_bytes = 0;
+        HIPCHK(where, hipMalloc(&t_ctx.dscratch, bytes));
+        t_ctx.dscratch_bytes = bytes;
+    }
+    return t_ctx.dscratch;
+}
+
+void *host_stage(const char *where, size_t bytes)
+{
+    if (t_ctx.hstage_bytes < bytes) {
+        if (t_ctx.hstage) HIPCHK(where, hipHostFree(t_ctx.hstage));
+        t_ctx.hstage = nullptr;
+        t_ctx.hstage_bytes = 0;
+        HIPCHK(where, hipHostMalloc(&t_ctx.hstage, bytes, hipHostMallocDefault));
+        t_ctx.hstage_bytes = bytes;
+    }
+    return t_ctx.hstage;
+}
+
+enum MemKind { MEM_HOST = 0, MEM_DEVICE = 1 };
+
+MemKind mem_kind(const void *p, int *dev)
+{
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void) hipGetLastError();  // unregistered pageable host memory
+        return MEM_HOST;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+        a.type == hipMemoryTypeUnified) {
+        if (dev) *dev = a.device;
+        return MEM_DEVICE;
+    }
+    return MEM_HOST;
+}
+
+bool ranges_overlap(const void *a, const void *b, size_t n)
+{
+    // byte-exact: the reference's OVERLAP_CHECK (src/reductions.c:27-30)
+    // adds a byte count to a typed pointer and over-detects by sizeof(T)
+    uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
+    return (x < y + n) && (y < x + n);
+}
+
+void fold_order(int me, int PE_start, int step, int PE_size, int *order)
+{
+    int k = 0;
+    order[k++] = me;
+    for (int i = 0, pe = PE_start; i < PE_size; i++, pe += step)
+        if (pe != me) order[k++] = pe;
+}
+
+// ------------------------------------------------------------- the paths
+
+struct Call {
+    const char *name;
+    int type, op;
+    void *target, *source;
+    int nreduce, PE_start, logPE_stride, PE_size;
+    long *pSync;
+    int me, step;
+    size_t nbytes;
+    PeOps ops;
+};
+
+void barrier(const Call &c)
+{
+    c.ops.barrier(c.PE_start, c.logPE_stride, c.PE_size, c.pSync);
+}
+
+bool p2p_sources(const Call &c, std::vector<const void *> &srcs)
+{
+    HeapEntry mine;
+    if (!heap_lookup(c.me, &mine)) return false;
+    const char *s = (const char *) c.source;
+    if (s < mine.base || s + c.nbytes > mine.base + mine.bytes) return false;
+    const size_t off = (size_t) (s - mine.base);
+    std::vector<int> order(c.PE_size);
+    fold_order(c.me, c.PE_start, c.step, c.PE_size, order.data());
+    srcs.resize(c.PE_size);
+    for (int k = 0; k < c.PE_size; k++) {
+        HeapEntry h;
+        if (!heap_lookup(order[k], &h) || off + c.nbytes > h.bytes) return false;
+        srcs[k] = h.base + off;
+    }
+    return true;
+}
+
+void run_p2p(const Call &c, const std::vector<const void *> &srcs)
+{
+    hipStream_t st = thread_stream(c.name);
+    // prior device work of this process that produced `source` must be done
+    HIPCHK(c.name, hipDeviceSynchronize());
+    barrier(c);  // src/reductions.c:82 -- every source is ready
+    const bool overlap = c.PE_size > 1 && ranges_overlap(c.target, c.source, c.nbytes);
+    void *out = overlap ? device_scratch(c.name, c.nbytes) : c.target;
+    hipError_t e = osgpu::launch_combine(c.type, c.op, out, srcs.data(), c.PE_size,
+                                         (size_t) c.nreduce, st);
+    if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
+    HIPCHK(c.name, hipStreamSynchronize(st));
+    barrier(c);  // src/reductions.c:113 -- peers are done reading my source
+    if (overlap) {
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c.name, hipStreamSynchronize(st));
+    }
+}
+
+bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *mult)
+{
+    *mult = 1;
+    switch (op) {
+    case OSGPU_OP_SUM: *rop = ncclSum; break;
+    case OSGPU_OP_PROD: *rop = ncclProd; break;
+    case OSGPU_OP_MAX: *rop = ncclMax; break;
+    case OSGPU_OP_MIN: *rop = ncclMin; break;
+    default: return false;
+    }
+    switch (type) {
+    case OSGPU_T_INT: *dt = ncclInt32; return true;
+    case OSGPU_T_LONG: case OSGPU_T_LONGLONG: *dt = ncclInt64; return true;
+    case OSGPU_T_FLOAT: *dt = ncclFloat32; return true;
+    case OSGPU_T_DOUBLE: *dt = ncclFloat64; return true;
+    case OSGPU_T_COMPLEXF: *dt = ncclFloat32; *mult = 2; return op == OSGPU_OP_SUM;
+    case OSGPU_T_COMPLEXD: *dt = ncclFloat64; *mult = 2; return op == OSGPU_OP_SUM;
+    }
+    return false;
+}
+
+bool rccl_usable(const Call &c)
+{
+    ncclDataType_t dt;
+    ncclRedOp_t rop;
+    size_t mult;
+    // the whole job only: a subset communicator would need ncclCommSplit,
+    // which every PE of the parent must call -- OpenSHMEM forbids
+    // non-members from calling a collective on an active set
+    return g_rccl.world && c.PE_start == 0 && c.step == 1 && c.PE_size == g_rccl.npes &&
+           c.me == g_rccl.me && rccl_types(c.type, c.op, &dt, &rop, &mult);
+}
+
+void run_rccl(const Call &c)
+{
+    ncclDataType_t dt;
+    ncclRedOp_t rop;
+    size_t mult;
+    rccl_types(c.type, c.op, &dt, &rop, &mult);
+    hipStream_t st = thread_stream(c.name);
+    HIPCHK(c.name, hipDeviceSynchronize());
+    const bool overlap = ranges_overlap(c.target, c.source, c.nbytes) && c.target != c.source;
+    void *out = overlap ? device_scratch(c.name, c.nbytes) : c.target;
+    ncclResult_t r = ncclAllReduce(c.source, out, (size_t) c.nreduce * mult, dt, rop,
+                                   g_rccl.world, st);
+    if (r != ncclSuccess) fatal(c.name, "ncclAllReduce: %s", ncclGetErrorString(r));
+    HIPCHK(c.name, hipStreamSynchronize(st));
+    if (overlap) {
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c.name, hipStreamSynchronize(st));
+    }
+}
+
+size_t host_chunk_bytes()
+{
+    const char *e = getenv("OSGPU_HOST_CHUNK_BYTES");
+    size_t b = e ? strtoull(e, nullptr, 0) : 0;
+    return b ? b : (size_t) 64 << 20;
+}
+
+// Host symmetric-heap arguments: the data arrives and leaves through host
+// memory (the UCX heap).  Peers' sources are pulled with the runtime's
+// shmem_getmem (src/putget.h:539-561), like the reference, but in large
+// chunks into pinned staging, then combined on the GPU.
+void run_host(const Call &c)
+{
+    if (!c.ops.getmem) fatal(c.name, "host-memory arguments need shmem_getmem");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        fatal(c.name, "no GPU visible: the combine runs only on the GPU");
+    hipStream_t st = thread_stream(c.name);
+    const size_t s = type_size(c.type);
+    const int P = c.PE_size;
+    std::vector<int> order(P);
+    fold_order(c.me, c.PE_start, c.step, P, order.data());
+
+    size_t chunk = host_chunk_bytes() / s;
+    if (chunk == 0) chunk = 1;
+    if (chunk > (size_t) c.nreduce) chunk = (size_t) c.nreduce;
+    chunk = (chunk + 1) & ~(size_t) 1;
+    const size_t cb = chunk * s;
+    // device: P input slots + 1 output slot; pinned: P input slots + output
+    char *dbuf = (char *) device_scratch(c.name, cb * (P + 1));
+    char *hbuf = (char *) host_stage(c.name, cb * (P + 1));
+    const bool overlap = P > 1 && ranges_overlap(c.target, c.source, c.nbytes);
+    char *result = overlap ? (char *) malloc(c.nbytes) : (char *) c.target;
+    if (!result) fatal(c.name, "out of memory for the temporary target");
+    std::vector<const void *> srcs(P);
+    for (int k = 0; k < P; k++) srcs[k] = dbuf + (size_t) k * cb;
+
+    barrier(c);  // src/reductions.c:82
+    for (size_t off = 0; off < (size_t) c.nreduce; off += chunk) {
+        const size_t n = ((size_t) c.nreduce - off) < chunk ? ((size_t) c.nreduce - off) : chunk;
+        const size_t nb = n * s;
+        for (int k = 0; k < P; k++) {
+            char *hk = hbuf + (size_t) k * cb;
+            const char *src = (const char *) c.source + off * s;
+            if (order[k] == c.me) memcpy(hk, src, nb);
+            else c.ops.getmem(hk, src, nb, order[k]);
+            HIPCHK(c.name, hipMemcpyAsync((void *) srcs[k], hk, nb, hipMemcpyHostToDevice, st));
+        }
+        char *dout = dbuf + (size_t) P * cb;
+        hipError_t e = osgpu::launch_combine(c.type, c.op, dout, srcs.data(), P, n, st);
+        if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
+        char *hout = hbuf + (size_t) P * cb;
+        HIPCHK(c.name, hipMemcpyAsync(hout, dout, nb, hipMemcpyDeviceToHost, st));
+        HIPCHK(c.name, hipStreamSynchronize(st));
+        memcpy(result + off * s, hout, nb);
+    }
+    barrier(c);  // src/reductions.c:113
+    if (overlap) {
+        memcpy(c.target, result, c.nbytes);  // src/reductions.c:114-119
+        free(result);
+    }
+}
+
+void to_all(const char *name, int type, int op, void *target, void *source, int nreduce,
+            int PE_start, int logPE_stride, int PE_size, void *pWrk, long *pSync)
+{
+    (void) pWrk;  // the combine needs no bounce buffer: peers are read directly
+    if (PE_size < 1 || PE_start < 0 || logPE_stride < 0 || logPE_stride > 30)
+        fatal(name, "invalid active set (PE_start=%d logPE_stride=%d PE_size=%d)", PE_start,
+              logPE_stride, PE_size);
+    Call c;
+    c.name = name;
+    c.type = type;
+    c.op = op;
+    c.target = target;
+    c.source = source;
+    c.nreduce = nreduce;
+    c.PE_start = PE_start;
+    c.logPE_stride = logPE_stride;
+    c.PE_size = PE_size;
+    c.pSync = pSync;
+    c.step = 1 << logPE_stride;
+    c.ops = pe_ops();
+    if (!c.ops.my_pe || !c.ops.barrier)
+        fatal(name, "no OpenSHMEM runtime: shmem_my_pe/shmem_barrier not found "
+                    "(link the OpenSHMEM library or call osgpu_set_pe_ops)");
+    c.me = c.ops.my_pe();
+    if (nreduce <= 0) {  // nothing to combine; the collective still syncs
+        barrier(c);
+        barrier(c);
+        return;
+    }
+    c.nbytes = type_size(type) * (size_t) nreduce;  // no int overflow (cf. :44)
+
+    int dt = -1, ds = -1;
+    MemKind kt = mem_kind(target, &dt), ks = mem_kind(source, &ds);
+    if (kt != ks)
+        fatal(name, "target and source must both be device or both be host memory");
+    if (kt == MEM_HOST) {
+        run_host(c);
+        return;
+    }
+    int cur = 0;
+    HIPCHK(name, hipGetDevice(&cur));
+    if (cur != dt) HIPCHK(name, hipSetDevice(dt));
+    const int mode = path_mode();
+    std::vector<const void *> srcs;
+    if (mode != OSGPU_PATH_RCCL && p2p_sources(c, srcs)) {
+        run_p2p(c, srcs);
+    } else if (mode != OSGPU_PATH_P2P && rccl_usable(c)) {
+        run_rccl(c);
+    } else {
+        fatal(name,
+              "device-resident arguments need either every active PE's device heap "
+              "registered (osgpu_heap_register) or an RCCL communicator covering the "
+              "active set with a supported type/op (path mode %d)",
+              mode);
+    }
+    if (cur != dt) HIPCHK(name, hipSetDevice(cur));
+}
+
+}  // namespace
+
+// ======================================================================
+// Part 1: the 44 entry points (pshmem_* strong, shmem_* weak aliases, as in
+// the reference's --enable-pshmem build, src/reductions.c:156-245)
+// ======================================================================
+
+#define OSGPU_DEFINE(_name, _type, _op, _tcode, _ocode)                        \
+    extern "C" void pshmem_##_name##_##_op##_to_all(                           \
+        _type *target, _type *source, int nreduce, int PE_start,               \
+        int logPE_stride, int PE_size, _type *pWrk, long *pSync)               \
+    {                                                                          \
+        to_all("shmem_" #_name "_" #_op "_to_all", _tcode, _ocode, target,     \
+               source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync); \
+    }                                                                          \
+    extern "C" void shmem_##_name##_##_op##_to_all(                            \
+        _type *target, _type *source, int nreduce, int PE_start,               \
+        int logPE_stride, int PE_size, _type *pWrk, long *pSync)               \
+        __attribute__((weak, alias("pshmem_" #_name "_" #_op "_to_all")));
+
+#define OSGPU_DEFINE_TYPE_OPS(_name, _type, _tcode)                            \
+    OSGPU_DEFINE(_name, _type, sum, _tcode, OSGPU_OP_SUM)                      \
+    OSGPU_DEFINE(_name, _type, prod, _tcode, OSGPU_OP_PROD)
+
+#define OSGPU_DEFINE_BITS(_name, _type, _tcode)                                \
+    OSGPU_DEFINE(_name, _type, and, _tcode, OSGPU_OP_AND)                      \
+    OSGPU_DEFINE(_name, _type, or, _tcode, OSGPU_OP_OR)                        \
+    OSGPU_DEFINE(_name, _type, xor, _tcode, OSGPU_OP_XOR)
+
+#define OSGPU_DEFINE_MINMAX(_name, _type, _tcode)                              \
+    OSGPU_DEFINE(_name, _type, max, _tcode, OSGPU_OP_MAX)                      \
+    OSGPU_DEFINE(_name, _type, min, _tcode, OSGPU_OP_MIN)
+
+typedef std::complex<float> osgpu_cf;
+typedef std::complex<double> osgpu_cd;
+
+OSGPU_DEFINE_TYPE_OPS(short, short, OSGPU_T_SHORT)
+OSGPU_DEFINE_TYPE_OPS(int, int, OSGPU_T_INT)
+OSGPU_DEFINE_TYPE_OPS(long, long, OSGPU_T_LONG)
+OSGPU_DEFINE_TYPE_OPS(longlong, long long, OSGPU_T_LONGLONG)
+OSGPU_DEFINE_TYPE_OPS(float, float, OSGPU_T_FLOAT)
+OSGPU_DEFINE_TYPE_OPS(double, double, OSGPU_T_DOUBLE)
+OSGPU_DEFINE_TYPE_OPS(longdouble, long double, OSGPU_T_LONGDOUBLE)
+OSGPU_DEFINE_TYPE_OPS(complexf, osgpu_cf, OSGPU_T_COMPLEXF)
+OSGPU_DEFINE_TYPE_OPS(complexd, osgpu_cd, OSGPU_T_COMPLEXD)
+OSGPU_DEFINE_BITS(short, short, OSGPU_T_SHORT)
+OSGPU_DEFINE_BITS(int, int, OSGPU_T_INT)
+OSGPU_DEFINE_BITS(long, long, OSGPU_T_LONG)
+OSGPU_DEFINE_BITS(longlong, long long, OSGPU_T_LONGLONG)
+OSGPU_DEFINE_MINMAX(short, short, OSGPU_T_SHORT)
+OSGPU_DEFINE_MINMAX(int, int, OSGPU_T_INT)
+OSGPU_DEFINE_MINMAX(long, long, OSGPU_T_LONG)
+OSGPU_DEFINE_MINMAX(longlong, long long, OSGPU_T_LONGLONG)
+OSGPU_DEFINE_MINMAX(float, float, OSGPU_T_FLOAT)
+OSGPU_DEFINE_MINMAX(double, double, OSGPU_T_DOUBLE)
+OSGPU_DEFINE_MINMAX(longdouble, long double, OSGPU_T_LONGDOUBLE)
+
+// ======================================================================
+// Part 2: control surface
+// ======================================================================
+
+extern "C" {
+
+int osgpu_set_pe_ops(const osgpu_pe_ops *ops)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!ops) {
+        g_ops = PeOps();
+        g_ops_set = false;
+        return OSGPU_OK;
+    }
+    if (!ops->my_pe || !ops->barrier) {
+        set_err("osgpu_set_pe_ops: my_pe and barrier are required");
+        return OSGPU_EINVAL;
+    }
+    g_ops.my_pe = ops->my_pe;
+    g_ops.n_pes = ops->n_pes;
+    g_ops.barrier = ops->barrier;
+    g_ops.getmem = ops->getmem;
+    g_ops_set = true;
+    return OSGPU_OK;
+}
+
+int osgpu_heap_register(int pe, void *base, size_t bytes)
+{
+    if (pe < 0 || !base || !bytes) {
+        set_err("osgpu_heap_register: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((size_t) pe >= g_heap.size()) g_heap.resize(pe + 1);
+    g_heap[pe].base = (char *) base;
+    g_heap[pe].bytes = bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_heap_unregister(int pe)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (pe < 0 || (size_t) pe >= g_heap.size()) return OSGPU_EINVAL;
+    g_heap[pe] = HeapEntry();
+    return OSGPU_OK;
+}
+
+void *osgpu_heap_translate(const void *addr, int from_pe, int to_pe)
+{
+    HeapEntry a, b;
+    if (!heap_lookup(from_pe, &a) || !heap_lookup(to_pe, &b)) return nullptr;
+    const char *p = (const char *) addr;
+    if (p < a.base || p >= a.base + a.bytes) return nullptr;
+    size_t off = (size_t) (p - a.base);
+    return off < b.bytes ? b.base + off : nullptr;
+}
+
+int osgpu_ipc_get_handle(void *dev_base, void *handle_out)
+{
+    static_assert(sizeof(hipIpcMemHandle_t) <= OSGPU_IPC_HANDLE_BYTES, "ipc handle size");
+    hipIpcMemHandle_t h;
+    hipError_t e = hipIpcGetMemHandle(&h, dev_base);
+    if (e != hipSuccess) {
+        set_err("hipIpcGetMemHandle: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    memset(handle_out, 0, OSGPU_IPC_HANDLE_BYTES);
+    memcpy(handle_out, &h, sizeof(h));
+    return OSGPU_OK;
+}
+
+void *osgpu_ipc_open(const void *handle)
+{
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    void *p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        set_err("hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+int osgpu_ipc_close(void *mapped)
+{
+    hipError_t e = hipIpcCloseMemHandle(mapped);
+    if (e != hipSuccess) {
+        set_err("hipIpcCloseMemHandle: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
+int osgpu_rccl_unique_id(void *uid_out)
+{
+    static_assert(sizeof(ncclUniqueId) == OSGPU_RCCL_UID_BYTES, "uid size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_err("ncclGetUniqueId: %s", ncclGetErrorString(r));
+        return OSGPU_ERCCL;
+    }
+    memcpy(uid_out, &id, sizeof(id));
+    return OSGPU_OK;
+}
+
+int osgpu_rccl_init(int npes, int me, const void *uid)
+{
+    if (g_rccl.world) return OSGPU_OK;
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof(id));
+    ncclComm_t comm;
+    ncclResult_t r = ncclCommInitRank(&comm, npes, id, me);
+    if (r != ncclSuccess) {
+        set_err("ncclCommInitRank: %s", ncclGetErrorString(r));
+        return OSGPU_ERCCL;
+    }
+    g_rccl.world = comm;
+    g_rccl.npes = npes;
+    g_rccl.me = me;
+    return OSGPU_OK;
+}
+
+int osgpu_rccl_finalize(void)
+{
+    if (!g_rccl.world) return OSGPU_OK;
+    ncclResult_t r = ncclCommDestroy(g_rccl.world);
+    g_rccl = Rccl();
+    return r == ncclSuccess ? OSGPU_OK : OSGPU_ERCCL;
+}
+
+int osgpu_set_path(int path)
+{
+    if (path < OSGPU_PATH_AUTO || path > OSGPU_PATH_RCCL) return OSGPU_EINVAL;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_path = path;
+    return OSGPU_OK;
+}
+
+int osgpu_set_stream(void *hip_stream)
+{
+    t_ctx.stream = (hipStream_t) hip_stream;
+    t_ctx.user_stream = hip_stream != nullptr;
+    if (!hip_stream) t_ctx.device = -1;
+    return OSGPU_OK;
+}
+
+void *osgpu_get_stream(void)
+{
+    return (void *) thread_stream("osgpu_get_stream");
+}
+
+int osgpu_combine(int type, int op, void *target, const void *const *srcs, int nsrc,
+                  size_t nelems, void *hip_stream)
+{
+    if (!has_op(type, op) || nsrc < 1 || !target || !srcs) {
+        set_err("osgpu_combine: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    hipStream_t st = hip_stream ? (hipStream_t) hip_stream : thread_stream("osgpu_combine");
+    hipError_t e = osgpu::launch_combine(type, op, target, srcs, nsrc, nelems, st);
+    if (e == hipErrorNotSupported) {
+        set_err("osgpu_combine: type %d op %d not supported on the GPU", type, op);
+        return OSGPU_ENOTSUP;
+    }
+    if (e != hipSuccess) {
+        set_err("osgpu_combine: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
+int osgpu_has_op(int type, int op) { return has_op(type, op) ? 1 : 0; }
+
+size_t osgpu_type_size(int type) { return type_size(type); }
+
+int osgpu_fold_order(int me, int PE_start, int logPE_stride, int PE_size, int *order_out)
+{
+    if (PE_size < 1 || logPE_stride < 0 || logPE_stride > 30 || !order_out)
+        return OSGPU_EINVAL;
+    const int step = 1 << logPE_stride;
+    bool member = false;
+    for (int i = 0; i < PE_size; i++) member |= (PE_start + i * step == me);
+    if (!member) return OSGPU_EINVAL;
+    fold_order(me, PE_start, step, PE_size, order_out);
+    return OSGPU_OK;
+}
+
+int osgpu_shard_range(long long nreduce, int PE_size, int idx, int elem_bytes, long long *lo,
+                      long long *hi)
+{
+    if (nreduce < 0 || PE_size < 1 || idx < 0 || idx >= PE_size || elem_bytes < 1 ||
+        elem_bytes > 16 || !lo || !hi)
+        return OSGPU_EINVAL;
+    // shard boundaries on 16-byte vector granules so every shard stays on
+    // the vector path; the last shard takes the ragged remainder
+    const long long g = elem_bytes >= 16 ? 1 : 16 / elem_bytes;
+    const long long granules = nreduce / g;
+    const long long base = granules / PE_size, rem = granules % PE_size;
+    const long long start = idx * base + (idx < rem ? idx : rem);
+    const long long cnt = base + (idx < rem ? 1 : 0);
+    *lo = start * g;
+    *hi = (idx == PE_size - 1) ? nreduce : (start + cnt) * g;
+    return OSGPU_OK;
+}
+
+const char *osgpu_last_error(void) { return g_err; }
+
+const char *osgpu_version(void) { return "osgpu_reduce 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+"""osgpu -- Python view of libosgpu_reduce.so (ctypes over the C ABI).
+
+The product is the C-ABI shared library built from ../csrc (declared in
+include/osgpu_reduce.h).  This module only loads it and describes its
+signatures so tests and bench.py can call the same entry points a C/Fortran
+OpenSHMEM application would (shmem_<TYPE>_<OP>_to_all, src/reductions.c:248-297
+of the reference).  It never computes anything itself, and it refuses to run
+without the compiled library: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libosgpu_reduce.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+REPO = os.path.dirname(PKG_DIR)
+HEADER = os.path.join(REPO, "include", "osgpu_reduce.h")
+
+TYPES = ["short", "int", "long", "longlong", "float", "double",
+         "longdouble", "complexf", "complexd"]
+OPS = ["sum", "prod", "and", "or", "xor", "max", "min"]
+CTYPE = {
+    "short": ctypes.c_short, "int": ctypes.c_int, "long": ctypes.c_long,
+    "longlong": ctypes.c_longlong, "float": ctypes.c_float,
+    "double": ctypes.c_double, "longdouble": ctypes.c_longdouble,
+    "complexf": ctypes.c_float * 2, "complexd": ctypes.c_double * 2,
+}
+PATH_AUTO, PATH_P2P, PATH_RCCL = 0, 1, 2
+
+
+def has_op(t: str, op: str) -> bool:
+    if op in ("sum", "prod"):
+        return True
+    if op in ("and", "or", "xor"):
+        return t in ("short", "int", "long", "longlong")
+    return op in ("max", "min") and t not in ("complexf", "complexd")
+
+
+ENTRY_POINTS = [f"shmem_{t}_{o}_to_all" for o in OPS for t in TYPES if has_op(t, o)]
+assert len(ENTRY_POINTS) == 44
+
+
+class PeOps(ctypes.Structure):
+    """struct osgpu_pe_ops (include/osgpu_reduce.h)"""
+    _fields_ = [
+        ("my_pe", ctypes.CFUNCTYPE(ctypes.c_int)),
+        ("n_pes", ctypes.CFUNCTYPE(ctypes.c_int)),
+        ("barrier", ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_long))),
+        ("getmem", ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_size_t, ctypes.c_int)),
+    ]
+
+
+def build(jobs: int = 8, quiet: bool = True) -> str:
+    """Compile the gfx950 library in-tree (make in csrc/)."""
+    kw = {}
+    if quiet:
+        kw = dict(stdout=subprocess.DEVNULL)
+    subprocess.run(["make", "-s", f"-j{jobs}"], cwd=CSRC, check=True, **kw)
+    return LIB_PATH
+
+
+_LIB = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libosgpu_reduce.so; raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() "
+                           "(the reduction has no CPU implementation)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    for name in ENTRY_POINTS:
+        for pfx in ("", "p"):
+            f = getattr(L, pfx + name)
+            f.argtypes = [vp, vp, i, i, i, i, vp, vp]
+            f.restype = None
+    L.osgpu_set_pe_ops.argtypes = [vp]
+    L.osgpu_heap_register.argtypes = [i, vp, sz]
+    L.osgpu_heap_unregister.argtypes = [i]
+    L.osgpu_heap_translate.argtypes = [vp, i, i]
+    L.osgpu_heap_translate.restype = vp
+    L.osgpu_ipc_get_handle.argtypes = [vp, vp]
+    L.osgpu_ipc_open.argtypes = [vp]
+    L.osgpu_ipc_open.restype = vp
+    L.osgpu_ipc_close.argtypes = [vp]
+    L.osgpu_rccl_unique_id.argtypes = [vp]
+    L.osgpu_rccl_init.argtypes = [i, i, vp]
+    L.osgpu_set_path.argtypes = [i]
+    L.osgpu_set_stream.argtypes = [vp]
+    L.osgpu_get_stream.restype = vp
+    L.osgpu_combine.argtypes = [i, i, vp, vp, i, sz, vp]
+    L.osgpu_has_op.argtypes = [i, i]
+    L.osgpu_type_size.argtypes = [i]
+    L.osgpu_type_size.restype = sz
+    L.osgpu_fold_order.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_int)]
+    L.osgpu_shard_range.argtypes = [ctypes.c_longlong, i, i, i,
+                                    ctypes.POINTER(ctypes.c_longlong),
+                                    ctypes.POINTER(ctypes.c_longlong)]
+    L.osgpu_last_error.restype = ctypes.c_char_p
+    L.osgpu_version.restype = ctypes.c_char_p
+    _LIB = L
+    return L
+
+
+def to_all(t: str, op: str):
+    """The ctypes function shmem_<t>_<op>_to_all."""
+    return getattr(load(), f"shmem_{t}_{op}_to_all")
+
+
+def combine(t: str, op: str, target: int, srcs, n: int, stream: int | None = None):
+    """Enqueue the combine kernel: target = fold(op, srcs...) (device ptrs)."""
+    L = load()
+    arr = (ctypes.c_void_p * len(srcs))(*srcs)
+    rc = L.osgpu_combine(TYPES.index(t), OPS.index(op), target, arr, len(srcs), n,
+                         stream)
+    if rc != 0:
+        raise RuntimeError(f"osgpu_combine({t},{op}) = {rc}: "
+                           f"{L.osgpu_last_error().decode()}")
+
+
+def fold_order(me, PE_start, logPE_stride, PE_size):
+    out = (ctypes.c_int * PE_size)()
+    rc = load().osgpu_fold_order(me, PE_start, logPE_stride, PE_size, out)
+    if rc != 0:
+        raise ValueError("PE not in active set")
+    return list(out)
+
+
+def shard_range(nreduce, PE_size, idx, elem_bytes):
+    lo, hi = ctypes.c_longlong(), ctypes.c_longlong()
+    rc = load().osgpu_shard_range(nreduce, PE_size, idx, elem_bytes,
+                                  ctypes.byref(lo), ctypes.byref(hi))
+    if rc != 0:
+        raise ValueError("bad shard arguments")
+    return lo.value, hi.value
+
+
+def header_symbols(path: str = HEADER):
+    """Function names declared in include/osgpu_reduce.h (expanding the
+    OSGPU_DECL_ALL macro for both prefixes)."""
+    import re
+    src = open(path).read()
+    names = set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(osgpu_\w+)\s*\(",
+                           src, re.M))
+    for pfx in ("shmem_", "pshmem_"):
+        for e in ENTRY_POINTS:
+            names.add(pfx + e[len("shmem_"):])
+    return sorted(names)

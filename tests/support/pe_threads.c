@@ -1,0 +1,118 @@
+/*
+ * pe_threads.c -- TEST INFRASTRUCTURE: an in-process OpenSHMEM PE runtime,
+ * one thread per PE ("threads-as-PEs").
+ *
+ * Supplies the PE services libosgpu_reduce.so takes from the OpenSHMEM
+ * runtime (struct osgpu_pe_ops): shmem_my_pe (src/ranks.c:17-23),
+ * shmem_n_pes, shmem_barrier over an active set (src/barrier.c:21-27) and
+ * shmem_getmem (src/putget.h:539-561) as a memcpy from the peer's host heap
+ * at the same offset (the base-offset translation of src/shmemc/comms.c:89-105).
+ * Only the transport is replaced; the library under test is the product.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+    int (*my_pe)(void);
+    int (*n_pes)(void);
+    void (*barrier)(int, int, int, long *);
+    void (*getmem)(void *, const void *, size_t, int);
+} pe_ops_t;
+
+#define MAXPE 64
+#define MAXBAR 64
+
+static int g_npes = 0;
+static __thread int t_me = -1;
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+
+typedef struct {
+    int used, start, stride, size;
+    pthread_barrier_t b;
+} bar_t;
+static bar_t g_bars[MAXBAR];
+static long g_bar_calls[MAXPE];
+
+static char *g_heap[MAXPE];
+static size_t g_heap_bytes[MAXPE];
+
+int pet_my_pe(void) { return t_me; }
+int pet_n_pes(void) { return g_npes; }
+
+void pet_set_me(int pe) { t_me = pe; }
+
+int pet_init(int npes)
+{
+    if (npes < 1 || npes > MAXPE) return -1;
+    pthread_mutex_lock(&g_mu);
+    for (int i = 0; i < MAXBAR; i++)
+        if (g_bars[i].used) {
+            pthread_barrier_destroy(&g_bars[i].b);
+            g_bars[i].used = 0;
+        }
+    memset(g_bar_calls, 0, sizeof(g_bar_calls));
+    memset(g_heap, 0, sizeof(g_heap));
+    memset(g_heap_bytes, 0, sizeof(g_heap_bytes));
+    g_npes = npes;
+    pthread_mutex_unlock(&g_mu);
+    return 0;
+}
+
+static pthread_barrier_t *find_bar(int start, int stride, int size)
+{
+    pthread_barrier_t *r = NULL;
+    pthread_mutex_lock(&g_mu);
+    for (int i = 0; i < MAXBAR && !r; i++)
+        if (g_bars[i].used && g_bars[i].start == start && g_bars[i].stride == stride &&
+            g_bars[i].size == size)
+            r = &g_bars[i].b;
+    for (int i = 0; i < MAXBAR && !r; i++)
+        if (!g_bars[i].used) {
+            g_bars[i].used = 1;
+            g_bars[i].start = start;
+            g_bars[i].stride = stride;
+            g_bars[i].size = size;
+            pthread_barrier_init(&g_bars[i].b, NULL, (unsigned) size);
+            r = &g_bars[i].b;
+        }
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}
+
+void pet_barrier(int PE_start, int logPE_stride, int PE_size, long *pSync)
+{
+    (void) pSync; /* left at SHMEM_SYNC_VALUE, as the reference's barrier leaves it */
+    if (t_me >= 0 && t_me < MAXPE) __atomic_add_fetch(&g_bar_calls[t_me], 1, __ATOMIC_RELAXED);
+    pthread_barrier_t *b = find_bar(PE_start, logPE_stride, PE_size);
+    if (!b) { fprintf(stderr, "pe_threads: barrier table full\n"); abort(); }
+    pthread_barrier_wait(b);
+}
+
+long pet_barrier_calls(int pe) { return (pe >= 0 && pe < MAXPE) ? g_bar_calls[pe] : -1; }
+
+int pet_register_host_heap(int pe, void *base, size_t bytes)
+{
+    if (pe < 0 || pe >= MAXPE) return -1;
+    g_heap[pe] = (char *) base;
+    g_heap_bytes[pe] = bytes;
+    return 0;
+}
+
+void pet_getmem(void *dest, const void *src, size_t n, int pe)
+{
+    const char *s = (const char *) src;
+    const int me = t_me;
+    if (me < 0 || pe < 0 || pe >= g_npes || !g_heap[me] || !g_heap[pe] || s < g_heap[me] ||
+        s + n > g_heap[me] + g_heap_bytes[me]) {
+        fprintf(stderr, "pe_threads: getmem of a non-symmetric address\n");
+        abort();
+    }
+    memcpy(dest, g_heap[pe] + (s - g_heap[me]), n);
+}
+
+static pe_ops_t g_table = {pet_my_pe, pet_n_pes, pet_barrier, pet_getmem};
+
+const void *pet_ops(void) { return &g_table; }

@@ -1,0 +1,139 @@
+"""team.py -- TEST INFRASTRUCTURE: drive libosgpu_reduce.so from a team of
+threads-as-PEs (tests/support/pe_threads.c supplies the PE services).
+
+Every PE owns a slice of one symmetric heap: on cuda:0 (device-resident
+path: the slices are registered with osgpu_heap_register so the library can
+address every PE's source) or in host memory (host-staged path: peers'
+sources are pulled with the runtime's getmem, as in the reference).  Each PE
+thread calls the real C entry point shmem_<type>_<op>_to_all, exactly like
+an OpenSHMEM program would.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PET_PATH = os.path.join(HERE, "libpe_threads.so")
+
+_PET = None
+
+
+def build_pet():
+    src = os.path.join(HERE, "pe_threads.c")
+    if (not os.path.exists(PET_PATH)
+            or os.path.getmtime(PET_PATH) < os.path.getmtime(src)):
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", PET_PATH, src,
+                        "-lpthread"], check=True)
+
+
+def pet():
+    global _PET
+    if _PET is None:
+        build_pet()
+        P = ctypes.CDLL(PET_PATH)
+        P.pet_ops.restype = ctypes.c_void_p
+        P.pet_register_host_heap.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        P.pet_barrier_calls.restype = ctypes.c_long
+        _PET = P
+    return _PET
+
+
+def _align(x, a=256):
+    return (x + a - 1) // a * a
+
+
+class Team:
+    """npes PEs, each with `heap_bytes` of symmetric heap (device or host)."""
+
+    def __init__(self, npes: int, heap_bytes: int, device: bool = True):
+        import osgpu
+        self.lib = osgpu.load()
+        self.osgpu = osgpu
+        self.pet = pet()
+        self.npes = npes
+        self.H = _align(heap_bytes)
+        self.device = device
+        assert self.pet.pet_init(npes) == 0
+        assert self.lib.osgpu_set_pe_ops(self.pet.pet_ops()) == 0
+        for pe in range(64):
+            self.lib.osgpu_heap_unregister(pe)
+        if device:
+            import torch
+            self.torch = torch
+            self.buf = torch.zeros(npes * self.H, dtype=torch.uint8, device="cuda:0")
+            self.base = self.buf.data_ptr()
+            for pe in range(npes):
+                assert self.lib.osgpu_heap_register(pe, self.base + pe * self.H, self.H) == 0
+        else:
+            self.hbuf = np.zeros(npes * self.H + 256, dtype=np.uint8)
+            a = self.hbuf.ctypes.data
+            self.hoff = (-a) % 256
+            self.base = a + self.hoff
+            for pe in range(npes):
+                assert self.pet.pet_register_host_heap(pe, self.base + pe * self.H, self.H) == 0
+
+    def ptr(self, pe: int, off: int) -> int:
+        return self.base + pe * self.H + off
+
+    def write(self, pe: int, off: int, arr: np.ndarray):
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        if raw.size == 0:
+            return
+        lo = pe * self.H + off
+        if self.device:
+            t = self.torch.from_numpy(raw.copy()).to("cuda:0")
+            self.buf[lo:lo + raw.size].copy_(t)
+        else:
+            self.hbuf[self.hoff + lo:self.hoff + lo + raw.size] = raw
+
+    def fill(self, pe: int, off: int, nbytes: int, byte: int):
+        lo = pe * self.H + off
+        if self.device:
+            self.buf[lo:lo + nbytes].fill_(byte)
+        else:
+            self.hbuf[self.hoff + lo:self.hoff + lo + nbytes] = byte
+
+    def read(self, pe: int, off: int, nbytes: int) -> np.ndarray:
+        lo = pe * self.H + off
+        if self.device:
+            self.torch.cuda.synchronize()
+            return self.buf[lo:lo + nbytes].cpu().numpy().copy()
+        return self.hbuf[self.hoff + lo:self.hoff + lo + nbytes].copy()
+
+    def run(self, t: str, op: str, target_off: int, source_off: int, nreduce: int,
+            PE_start: int = 0, logPE_stride: int = 0, PE_size: int | None = None,
+            members=None):
+        """Every PE of the active set calls shmem_<t>_<op>_to_all on its own
+        thread (blocking collective)."""
+        if PE_size is None:
+            PE_size = self.npes
+        step = 1 << logPE_stride
+        if members is None:
+            members = [PE_start + i * step for i in range(PE_size)]
+        fn = self.osgpu.to_all(t, op)
+        psync = (ctypes.c_long * 128)()
+        pwrk = (ctypes.c_byte * 4096)()
+        errs = []
+
+        def body(pe):
+            try:
+                self.pet.pet_set_me(pe)
+                fn(self.ptr(pe, target_off), self.ptr(pe, source_off), nreduce,
+                   PE_start, logPE_stride, PE_size, ctypes.addressof(pwrk),
+                   ctypes.addressof(psync))
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        ths = [threading.Thread(target=body, args=(pe,)) for pe in members]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errs:
+            raise errs[0]
+        assert all(v == 0 for v in psync), "pSync must be left at SHMEM_SYNC_VALUE"

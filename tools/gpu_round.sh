@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU parity tests, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash/abort/timeout (exit status
+# other than 0 or 1) ends the script so nothing else touches the GPU.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME SECONDS CMD...
+    local name=$1 secs=$2; shift 2
+    echo "== $name: $*" | tee -a gpurun_out/steps.log
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+    tail -5 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+for s in ${STEPS:-smoke tests bench prof}; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 ;;
+  esac
+done
+echo "all steps done"
