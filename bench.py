@@ -74,14 +74,17 @@ def cpu_baseline(n):
     import numpy as np
     import oracle as O
     src = O.team_inputs("double", 2, n, 0x5EED, "unit12")
+    # size the repetition count for ~10 s of CPU work (bounded sample)
+    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True)
+    reps = max(3, min(200, int(10.0 / max(probe, 1e-3))))
     t0 = time.time()
-    sec = O.cpu_baseline("double", "sum", src, reps=3, pin=True)
+    sec = O.cpu_baseline("double", "sum", src, reps=reps, pin=True)
     wall = time.time() - t0
     B = 2 * 3 * n * 8  # two PE results, each (K+1)*n*8
     return {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
             "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
-                       f"2 PEs (pthreads pinned to cores 0-1), nreduce={n}, median of 3 "
-                       f"after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
+                       f"2 PEs (pthreads pinned to cores 0-1), nreduce={n}, median of "
+                       f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
                        f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
 
 
@@ -118,6 +121,7 @@ def bench_single(args):
     stream = torch.cuda.Stream(device=dev)
     srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
     sp = ctypes.c_void_p(stream.cuda_stream)
+    torch.cuda.synchronize()  # inputs were written on torch's default stream
 
     def step():
         rc = L.osgpu_combine(5, 0, out.data_ptr(), srcs, 2, n, sp)

@@ -21,8 +21,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
+    tune)  step tune 300 ./tools/tune_combine ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
-           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 ;;
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+           python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $((64<<20)) gpurun_out/traffic.json ;;
   esac
 done
 echo "all steps done"
