@@ -275,7 +275,11 @@ def special_values(t: str) -> np.ndarray:
     raw = arr.view(np.uint8).reshape(-1, 16).copy()
     extra = []
     for sig, se in ((0xC000000000000123, 0x7FFF), (0x8000000000000001, 0x7FFF),
-                    (0xA000000000000000, 0xFFFF)):
+                    (0xA000000000000000, 0xFFFF),
+                    # x87 encodings with no IEEE counterpart: unnormal,
+                    # pseudo-denormal, pseudo-infinity, pseudo-NaN
+                    (0x4000000000000000, 0x3FFF), (0x8000000000000001, 0x0000),
+                    (0x0000000000000000, 0x7FFF), (0x4000000000000001, 0xFFFF)):
         row = np.zeros(16, dtype=np.uint8)
         row[:8] = np.frombuffer(int(sig).to_bytes(8, "little"), dtype=np.uint8)
         row[8:10] = np.frombuffer(int(se).to_bytes(2, "little"), dtype=np.uint8)

@@ -17,6 +17,16 @@ enum TypeCode {
 hipError_t launch_combine(int type, int op, void *out, const void *const *srcs, int k,
                           size_t n, hipStream_t s);
 
+// Owner-computes team combine over an active set of P PEs (2 <= P <= 8):
+// for i < n, dsts[q][i] = fold of srcs[*][i] in PE q's order (q first, then
+// ascending, skipping q).  srcs/dsts indexed by position in the active set
+// and already offset to this PE's shard.
+constexpr int kMaxTeam = 8;
+hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                       size_t n, hipStream_t s);
+hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,
+                                  size_t n, hipStream_t s);
+
 // x87 80-bit extended combine (soft-float on the GPU), longdouble.hip
 hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, size_t n,
                              hipStream_t s);

@@ -1,11 +1,159 @@
-// longdouble.hip -- x87 80-bit extended reduce-to-all combine (placeholder).
+// longdouble.hip -- shmem_longdouble_{sum,prod,max,min}_to_all combine on gfx950.
+//
+// The reference folds `long double` with x87 instructions (fadd / fmul /
+// fcomi from src/shmemu/miscops.c:30,98 compiled for x86-64), i.e. 80-bit
+// extended precision: 64-bit significand with an explicit integer bit,
+// 15-bit exponent, round-to-nearest-even, gradual underflow.  The GPU has
+// no such type, so this file is a bit-exact x87 soft-float:
+//
+//   * encodings: zero, denormal (e=0, J=0), pseudo-denormal (e=0, J=1; the
+//     same value as e=1), normal, infinity, QNaN/SNaN; "unsupported"
+//     encodings (unnormal: 0<e<0x7fff with J=0; pseudo-infinity/pseudo-NaN:
+//     e=0x7fff with J=0) are invalid operands;
+//   * add/mul: exact 128-bit intermediate, one RNE rounding to 64 bits (or
+//     to the denormal grid), overflow to infinity;
+//   * NaN results (probed through the reference's own compiled ops, see
+//     tests/test_oracle.py and DESIGN.md): an invalid operand or invalid
+//     operation gives the default NaN ffff:c000000000000000 (even beside a
+//     NaN operand); otherwise the NaN with the larger 64-bit significand wins,
+//     quieted; equal significands -> positive sign;
+//   * min/max: `a<b?a:b` / `a>b?a:b` with fcomi semantics: any NaN or
+//     unsupported operand is unordered (-> b), +0 == -0, selection returns
+//     the original encoding.
+// Storage: 16 bytes per element (x86-64 ABI); bytes 10..15 are padding and
+// are written as zero.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
 #include "combine.hpp"
+#include "x87.hpp"
 
 namespace osgpu {
+namespace x87 {
 
-hipError_t launch_longdouble(int, void *, const void *const *, int, size_t, hipStream_t)
+__device__ __forceinline__ X80 load(const unsigned char *p)
 {
-    return hipErrorNotSupported;
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
+    return X80{q[0], (uint32_t) (q[1] & 0xffffu)};
+}
+
+__device__ __forceinline__ void store(unsigned char *p, X80 x)
+{
+    uint64_t *q = reinterpret_cast<uint64_t *>(p);
+    q[0] = x.m;
+    q[1] = (uint64_t) (x.se & 0xffffu);          // padding bytes written as zero
+}
+
+template <int OP>
+__device__ __forceinline__ X80 apply(X80 a, X80 b)
+{
+    if (OP == 0) return add(a, b);
+    if (OP == 1) return mul(a, b);
+    if (OP == 5) return less(b, a) ? a : b;      // max: a > b ? a : b
+    return less(a, b) ? a : b;                   // min: a < b ? a : b
+}
+
+constexpr int kMaxIn = 8;
+
+struct LdInputs {
+    const unsigned char *p[kMaxIn];
+};
+
+template <int OP>
+__global__ __launch_bounds__(256) void ld_combine_kernel(unsigned char *out, LdInputs in,
+                                                         int k, size_t n)
+{
+    const size_t stride = (size_t) gridDim.x * blockDim.x;
+    for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        X80 acc = load(in.p[0] + 16 * i);
+        for (int j = 1; j < k; j++) acc = apply<OP>(acc, load(in.p[j] + 16 * i));
+        store(out + 16 * i, acc);
+    }
+}
+
+}  // namespace x87
+
+hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, size_t n,
+                             hipStream_t s)
+{
+    if (op != 0 && op != 1 && op != 5 && op != 6) return hipErrorInvalidValue;
+    for (int j = 0; j < k; j++)
+        if (((uintptr_t) srcs[j] & 7) != 0) return hipErrorInvalidValue;
+    if (((uintptr_t) out & 7) != 0) return hipErrorInvalidValue;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    if (blocks == 0) blocks = 1;
+    // chunks of up to 8 inputs, left to right: out = fold(out, next 7 ...)
+    int done = 0;
+    bool first = true;
+    while (done < k) {
+        x87::LdInputs in;
+        int m = 0;
+        if (!first) in.p[m++] = (const unsigned char *) out;
+        while (m < x87::kMaxIn && done < k) in.p[m++] = (const unsigned char *) srcs[done++];
+        first = false;
+        switch (op) {
+        case 0: hipLaunchKernelGGL(x87::ld_combine_kernel<0>, dim3((unsigned) blocks), dim3(256), 0, s,
+                                   (unsigned char *) out, in, m, n); break;
+        case 1: hipLaunchKernelGGL(x87::ld_combine_kernel<1>, dim3((unsigned) blocks), dim3(256), 0, s,
+                                   (unsigned char *) out, in, m, n); break;
+        case 5: hipLaunchKernelGGL(x87::ld_combine_kernel<5>, dim3((unsigned) blocks), dim3(256), 0, s,
+                                   (unsigned char *) out, in, m, n); break;
+        default: hipLaunchKernelGGL(x87::ld_combine_kernel<6>, dim3((unsigned) blocks), dim3(256), 0, s,
+                                    (unsigned char *) out, in, m, n); break;
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+namespace x87 {
+
+struct LdTeam {
+    const unsigned char *src[kMaxTeam];
+    unsigned char *dst[kMaxTeam];
+};
+
+// owner-computes form (team.hip): every PE's own fold order, P^2 soft ops
+template <int OP>
+__global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, int P, size_t n)
+{
+    const size_t stride = (size_t) gridDim.x * blockDim.x;
+    for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        X80 x[kMaxTeam];
+        for (int p = 0; p < P; p++) x[p] = load(a.src[p] + 16 * i);
+        for (int q = 0; q < P; q++) {
+            X80 acc = x[q];
+            for (int j = 0; j < P; j++)
+                if (j != q) acc = apply<OP>(acc, x[j]);
+            store(a.dst[q] + 16 * i, acc);
+        }
+    }
+}
+
+}  // namespace x87
+
+hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,
+                                  size_t n, hipStream_t s)
+{
+    if (P < 2 || P > kMaxTeam) return hipErrorInvalidValue;
+    x87::LdTeam a;
+    for (int p = 0; p < P; p++) {
+        a.src[p] = (const unsigned char *) srcs[p];
+        a.dst[p] = (unsigned char *) dsts[p];
+        if ((((uintptr_t) srcs[p]) | ((uintptr_t) dsts[p])) & 7) return hipErrorInvalidValue;
+    }
+    size_t blocks = (n + 255) / 256;
+    blocks = blocks > 16384 ? 16384 : (blocks ? blocks : 1);
+    switch (op) {
+    case 0: hipLaunchKernelGGL(x87::ld_team_kernel<0>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
+    case 1: hipLaunchKernelGGL(x87::ld_team_kernel<1>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
+    case 5: hipLaunchKernelGGL(x87::ld_team_kernel<5>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
+    case 6: hipLaunchKernelGGL(x87::ld_team_kernel<6>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace osgpu

@@ -163,6 +163,7 @@ int path_mode()
         const char *e = getenv("OSGPU_REDUCE_PATH");
         if (e && !strcmp(e, "p2p")) g_path = OSGPU_PATH_P2P;
         if (e && !strcmp(e, "rccl")) g_path = OSGPU_PATH_RCCL;
+        if (e && !strcmp(e, "pull")) g_path = OSGPU_PATH_PULL;
     }
     return g_path;
 }
@@ -283,6 +284,58 @@ bool p2p_sources(const Call &c, std::vector<const void *> &srcs)
         srcs[k] = h.base + off;
     }
     return true;
+}
+
+// Owner-computes team path (team.hip): needs both source and target inside
+// every active PE's registered heap at the same offsets (symmetric), no
+// overlap between them, and 2 <= PE_size <= 8.  Fills srcs/dsts in active-set
+// order and returns this PE's index, or -1.
+int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *> &dsts)
+{
+    if (c.PE_size < 2 || c.PE_size > osgpu::kMaxTeam) return -1;
+    if (ranges_overlap(c.target, c.source, c.nbytes)) return -1;
+    HeapEntry mine;
+    if (!heap_lookup(c.me, &mine)) return -1;
+    const char *s = (const char *) c.source, *t = (const char *) c.target;
+    if (s < mine.base || s + c.nbytes > mine.base + mine.bytes) return -1;
+    if (t < mine.base || t + c.nbytes > mine.base + mine.bytes) return -1;
+    const size_t os = (size_t) (s - mine.base), ot = (size_t) (t - mine.base);
+    srcs.resize(c.PE_size);
+    dsts.resize(c.PE_size);
+    int idx = -1;
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        HeapEntry h;
+        if (!heap_lookup(pe, &h) || os + c.nbytes > h.bytes || ot + c.nbytes > h.bytes)
+            return -1;
+        srcs[i] = h.base + os;
+        dsts[i] = h.base + ot;
+        if (pe == c.me) idx = i;
+    }
+    return idx;
+}
+
+void run_team(const Call &c, const std::vector<const void *> &srcs,
+              const std::vector<void *> &dsts, int idx)
+{
+    hipStream_t st = thread_stream(c.name);
+    const size_t s = type_size(c.type);
+    long long lo = 0, hi = 0;
+    osgpu_shard_range(c.nreduce, c.PE_size, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
+    std::vector<const void *> sp(c.PE_size);
+    std::vector<void *> dp(c.PE_size);
+    for (int i = 0; i < c.PE_size; i++) {
+        sp[i] = (const char *) srcs[i] + (size_t) lo * s;
+        dp[i] = (char *) dsts[i] + (size_t) lo * s;
+    }
+    HIPCHK(c.name, hipDeviceSynchronize());
+    barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
+    if (hi > lo) {
+        hipError_t e = osgpu::launch_team(c.type, c.op, c.PE_size, dp.data(), sp.data(),
+                                          (size_t) (hi - lo), st);
+        if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
+    }
+    HIPCHK(c.name, hipStreamSynchronize(st));
+    barrier(c);  // src/reductions.c:113 -- every shard of my target is written
 }
 
 void run_p2p(const Call &c, const std::vector<const void *> &srcs)
@@ -464,9 +517,14 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     if (cur != dt) HIPCHK(name, hipSetDevice(dt));
     const int mode = path_mode();
     std::vector<const void *> srcs;
-    if (mode != OSGPU_PATH_RCCL && p2p_sources(c, srcs)) {
+    std::vector<void *> dsts;
+    int idx = -1;
+    if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_P2P) &&
+        (idx = team_ptrs(c, srcs, dsts)) >= 0) {
+        run_team(c, srcs, dsts, idx);
+    } else if (mode != OSGPU_PATH_RCCL && p2p_sources(c, srcs)) {
         run_p2p(c, srcs);
-    } else if (mode != OSGPU_PATH_P2P && rccl_usable(c)) {
+    } else if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_RCCL) && rccl_usable(c)) {
         run_rccl(c);
     } else {
         fatal(name,
@@ -669,7 +727,7 @@ int osgpu_rccl_finalize(void)
 
 int osgpu_set_path(int path)
 {
-    if (path < OSGPU_PATH_AUTO || path > OSGPU_PATH_RCCL) return OSGPU_EINVAL;
+    if (path < OSGPU_PATH_AUTO || path > OSGPU_PATH_PULL) return OSGPU_EINVAL;
     std::lock_guard<std::mutex> lk(g_mu);
     g_path = path;
     return OSGPU_OK;

@@ -1,0 +1,226 @@
+// team.hip -- owner-computes reduce-to-all for a whole active set.
+//
+// The reference makes every PE pull every other PE's whole source
+// (src/reductions.c:84-111): P*(P-1)*N elements cross the PE boundary and
+// every PE reads P*N.  Here PE g (index g of the active set) owns the element
+// shard [lo_g, hi_g) of ALL targets (targets are symmetric objects in
+// OpenSHMEM 1.4): it reads shard g of the P sources once, computes the P
+// per-PE results -- each in that PE's own fold order, op(op(x_q, x_0), x_1)
+// ... skipping q (src/reductions.c:79-111) -- and writes shard g of every
+// PE's target.  Per call the team moves 2*P*N*s bytes instead of
+// P*(P+1)*N*s; across GPUs each PE exchanges (P-1)/P * N * s each way, the
+// traffic of a reduce-scatter + all-gather, and the result stays bit-exact.
+//
+// Order-independent ops (every integer op) fold once and store P copies.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <type_traits>
+
+#include "combine.hpp"
+#include "elem_ops.hpp"
+
+#pragma clang fp contract(off)
+
+namespace osgpu {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+union TVec {
+    u32x4 v;
+    T e[16 / sizeof(T)];
+};
+
+template <typename T, int P>
+struct TeamPtrs {
+    const T *src[P];
+    T *dst[P];
+};
+
+constexpr int kTeamBlock = 256;
+
+template <typename T, int OP, int P, bool ORDERED>
+__device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
+{
+    if (ORDERED) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            T acc = x[q];
+#pragma unroll
+            for (int j = 0; j < P; j++)
+                if (j != q) acc = Elem<T, OP>::f(acc, x[j]);
+            r[q] = acc;
+        }
+    } else {
+        T acc = x[0];
+#pragma unroll
+        for (int j = 1; j < P; j++) acc = Elem<T, OP>::f(acc, x[j]);
+#pragma unroll
+        for (int q = 0; q < P; q++) r[q] = acc;
+    }
+}
+
+template <typename T, int OP, int P, bool ORDERED>
+__global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, size_t nvec,
+                                                              size_t head, size_t tail_start,
+                                                              int nedge)
+{
+    constexpr int W = 16 / sizeof(T);
+    constexpr int U = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
+    if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
+        const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
+        T x[P], r[P];
+#pragma unroll
+        for (int p = 0; p < P; p++) x[p] = a.src[p][e];
+        team_fold<T, OP, P, ORDERED>(x, r);
+#pragma unroll
+        for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
+    }
+    const size_t t0 = (size_t) blockIdx.x * (kTeamBlock * U) + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t j = t0 + (size_t) u * kTeamBlock;
+        if (j >= nvec) break;
+        TVec<T> in[P];
+#pragma unroll
+        for (int p = 0; p < P; p++)
+            in[p].v = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4 *>(a.src[p] + head) + j);
+        TVec<T> out[P];
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            T x[P], r[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) x[p] = in[p].e[w];
+            team_fold<T, OP, P, ORDERED>(x, r);
+#pragma unroll
+            for (int p = 0; p < P; p++) out[p].e[w] = r[p];
+        }
+#pragma unroll
+        for (int p = 0; p < P; p++)
+            __builtin_nontemporal_store(out[p].v, reinterpret_cast<u32x4 *>(a.dst[p] + head) + j);
+    }
+}
+
+template <typename T, int OP, int P, bool ORDERED>
+__global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> a, size_t n)
+{
+    const size_t stride = (size_t) gridDim.x * kTeamBlock;
+    for (size_t i = (size_t) blockIdx.x * kTeamBlock + threadIdx.x; i < n; i += stride) {
+        T x[P], r[P];
+#pragma unroll
+        for (int p = 0; p < P; p++) x[p] = a.src[p][i];
+        team_fold<T, OP, P, ORDERED>(x, r);
+#pragma unroll
+        for (int p = 0; p < P; p++) a.dst[p][i] = r[p];
+    }
+}
+
+template <typename T, int OP, int P>
+static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size_t n,
+                                hipStream_t s)
+{
+    // integer ops are order-independent (wrapping ring / lattice ops); every
+    // floating-point op, min/max included (NaN, signed zero), is not
+    constexpr bool ORDERED = !std::is_integral<T>::value;
+    TeamPtrs<T, P> a;
+    const uintptr_t phase = (uintptr_t) srcs[0] & 15;
+    bool same = (phase % sizeof(T)) == 0;
+    for (int p = 0; p < P; p++) {
+        a.src[p] = static_cast<const T *>(srcs[p]);
+        a.dst[p] = static_cast<T *>(dsts[p]);
+        same = same && (((uintptr_t) srcs[p] & 15) == phase) && (((uintptr_t) dsts[p] & 15) == phase);
+    }
+    if (!same) {
+        size_t blocks = (n + kTeamBlock - 1) / kTeamBlock;
+        blocks = blocks > 8192 ? 8192 : (blocks ? blocks : 1);
+        hipLaunchKernelGGL((team_scalar_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
+                           dim3(kTeamBlock), 0, s, a, n);
+        return hipGetLastError();
+    }
+    constexpr int W = 16 / sizeof(T);
+    constexpr int U = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
+    size_t head = phase ? (16 - phase) / sizeof(T) : 0;
+    if (head > n) head = n;
+    const size_t nvec = (n - head) / W;
+    const size_t tail_start = head + nvec * W;
+    const int nedge = (int) (head + (n - tail_start));
+    size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
+                       dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge);
+    return hipGetLastError();
+}
+
+template <typename T, int OP>
+static hipError_t team_launch_op(int P, void *const *d, const void *const *sr, size_t n,
+                                 hipStream_t s)
+{
+    switch (P) {
+    case 2: return team_launch_p<T, OP, 2>(d, sr, n, s);
+    case 3: return team_launch_p<T, OP, 3>(d, sr, n, s);
+    case 4: return team_launch_p<T, OP, 4>(d, sr, n, s);
+    case 5: return team_launch_p<T, OP, 5>(d, sr, n, s);
+    case 6: return team_launch_p<T, OP, 6>(d, sr, n, s);
+    case 7: return team_launch_p<T, OP, 7>(d, sr, n, s);
+    case 8: return team_launch_p<T, OP, 8>(d, sr, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+#define TEAM_CASE(OPC)                                                         \
+    case OPC: return team_launch_op<T, OPC>(P, d, sr, n, s);
+
+template <typename T>
+static hipError_t team_int(int op, int P, void *const *d, const void *const *sr, size_t n,
+                           hipStream_t s)
+{
+    switch (op) {
+        TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD) TEAM_CASE(OP_AND) TEAM_CASE(OP_OR)
+        TEAM_CASE(OP_XOR) TEAM_CASE(OP_MAX) TEAM_CASE(OP_MIN)
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t team_real(int op, int P, void *const *d, const void *const *sr, size_t n,
+                            hipStream_t s)
+{
+    switch (op) {
+        TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD) TEAM_CASE(OP_MAX) TEAM_CASE(OP_MIN)
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t team_cplx(int op, int P, void *const *d, const void *const *sr, size_t n,
+                            hipStream_t s)
+{
+    switch (op) {
+        TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD)
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                       size_t n, hipStream_t s)
+{
+    if (P < 2 || P > kMaxTeam) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    switch (type) {
+    case T_SHORT: return team_int<int16_t>(op, P, dsts, srcs, n, s);
+    case T_INT: return team_int<int32_t>(op, P, dsts, srcs, n, s);
+    case T_LONG:
+    case T_LONGLONG: return team_int<int64_t>(op, P, dsts, srcs, n, s);
+    case T_FLOAT: return team_real<float>(op, P, dsts, srcs, n, s);
+    case T_DOUBLE: return team_real<double>(op, P, dsts, srcs, n, s);
+    case T_COMPLEXF: return team_cplx<cfloat>(op, P, dsts, srcs, n, s);
+    case T_COMPLEXD: return team_cplx<cdouble>(op, P, dsts, srcs, n, s);
+    case T_LONGDOUBLE: return launch_team_longdouble(op, P, dsts, srcs, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace osgpu

@@ -1,0 +1,193 @@
+// x87.hpp -- bit-exact x87 80-bit extended arithmetic (host + device).
+// Used by longdouble.hip on the GPU; the identical code is compiled for the
+// host only by tests/support (to check it against the reference's own x87
+// ops on millions of inputs before it runs on an MI355X).
+// See longdouble.hip for the semantics.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef OSGPU_HD
+#define OSGPU_HD __host__ __device__
+#endif
+
+namespace osgpu {
+namespace x87 {
+
+typedef unsigned __int128 u128;
+
+struct X80 {
+    uint64_t m;   // significand, bit 63 = explicit integer bit J
+    uint32_t se;  // bit 15 sign, bits 0..14 biased exponent
+};
+
+enum Cls { C_ZERO, C_FIN, C_INF, C_QNAN, C_SNAN, C_BAD };
+
+constexpr int kBias = 16383;
+constexpr uint32_t kEmax = 0x7fff;
+
+OSGPU_HD inline X80 defnan() { return X80{0xC000000000000000ull, 0xFFFFu}; }
+
+OSGPU_HD inline Cls classify(X80 x)
+{
+    const uint32_t e = x.se & kEmax;
+    const bool j = (x.m >> 63) != 0;
+    if (e == kEmax) {
+        if (!j) return C_BAD;                      // pseudo-infinity / pseudo-NaN
+        if ((x.m << 1) == 0) return C_INF;
+        return ((x.m >> 62) & 1) ? C_QNAN : C_SNAN;
+    }
+    if (e == 0) return x.m == 0 ? C_ZERO : C_FIN;    // denormal or pseudo-denormal
+    return j ? C_FIN : C_BAD;                        // unnormal is unsupported
+}
+
+OSGPU_HD inline bool is_nan(Cls c) { return c == C_QNAN || c == C_SNAN; }
+
+OSGPU_HD inline int clz128(u128 v)
+{
+    const uint64_t hi = (uint64_t) (v >> 64), lo = (uint64_t) v;
+    return hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);
+}
+
+// NaN propagation with at least one NaN operand and no unsupported one
+OSGPU_HD inline X80 nan_pick(X80 a, Cls ca, X80 b, Cls cb)
+{
+    X80 r;
+    if (is_nan(ca) && is_nan(cb)) {
+        if (a.m > b.m) r = a;
+        else if (b.m > a.m) r = b;
+        else r = X80{a.m, (a.se & b.se)};        // tie: positive if either is
+    } else {
+        r = is_nan(ca) ? a : b;
+    }
+    r.m |= 1ull << 62;                           // quiet
+    return r;
+}
+
+// Round a value sign * S * 2^(E - bias - 127), S normalised with bit 127 set
+// (or S == 0), to x87 extended and encode it.
+OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
+{
+    if (S == 0) return X80{0, sign << 15};
+    if (E < 1) {                                 // gradual underflow
+        const int sh = 1 - E;
+        if (sh >= 128) {
+            S = 1;                               // sticky only
+        } else {
+            const bool sticky = (S << (128 - sh)) != 0;
+            S = (S >> sh) | (u128) (sticky ? 1 : 0);
+        }
+        E = 1;
+    }
+    uint64_t hi = (uint64_t) (S >> 64);
+    const uint64_t lo = (uint64_t) S;
+    const bool half = (lo >> 63) != 0;
+    const bool rest = (lo << 1) != 0;
+    if (half && (rest || (hi & 1))) {
+        hi += 1;
+        if (hi == 0) {                           // carried out of 64 bits
+            hi = 1ull << 63;
+            E += 1;
+        }
+    }
+    if (E >= (int) kEmax) return X80{1ull << 63, (sign << 15) | kEmax};  // overflow -> inf
+    const uint32_t e = (hi >> 63) ? (uint32_t) E : 0u;                    // denormal if J=0
+    return X80{hi, (sign << 15) | e};
+}
+
+OSGPU_HD inline X80 add(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD) return defnan();
+    if (is_nan(ca) || is_nan(cb)) return nan_pick(a, ca, b, cb);
+    const uint32_t sa = (a.se >> 15) & 1, sb = (b.se >> 15) & 1;
+    if (ca == C_INF || cb == C_INF) {
+        if (ca == C_INF && cb == C_INF) return sa == sb ? a : defnan();
+        return ca == C_INF ? a : b;
+    }
+    if (ca == C_ZERO && cb == C_ZERO) return X80{0, (sa & sb) << 15};
+    int Ea = (int) (a.se & kEmax), Eb = (int) (b.se & kEmax);
+    Ea = Ea ? Ea : 1;
+    Eb = Eb ? Eb : 1;
+    uint64_t ma = a.m, mb = b.m;
+    uint32_t sign = sa;
+    if (cb == C_ZERO) { mb = 0; Eb = Ea; }
+    if (ca == C_ZERO) { ma = 0; Ea = Eb; }
+    // order by magnitude: |a| >= |b|
+    if (Eb > Ea || (Eb == Ea && mb > ma)) {
+        uint64_t tm = ma; ma = mb; mb = tm;
+        int te = Ea; Ea = Eb; Eb = te;
+        sign = sb;
+    }
+    const int d = Ea - Eb;
+    const u128 A = (u128) ma << 64;
+    u128 B = (u128) mb << 64;
+    if (d >= 128) {
+        B = (mb != 0) ? 1 : 0;
+    } else if (d > 0) {
+        const bool sticky = (B << (128 - d)) != 0;
+        B = (B >> d) | (u128) (sticky ? 1 : 0);
+    }
+    int E = Ea;
+    u128 S;
+    if (sa == sb) {
+        S = A + B;
+        if (S < A) {                             // carry out of bit 127
+            S = (S >> 1) | (S & 1) | ((u128) 1 << 127);
+            E += 1;
+        }
+    } else {
+        S = A - B;
+        if (S == 0) return X80{0, 0};            // exact cancellation: +0 (RNE)
+    }
+    const int lz = clz128(S);
+    S <<= lz;
+    E -= lz;
+    // value = S * 2^(E - bias - 127): the exponent convention above treats
+    // the 128-bit S as significand bits 127..0 with J at 127
+    return round_pack(sign, E, S);
+}
+
+OSGPU_HD inline X80 mul(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD) return defnan();
+    if (is_nan(ca) || is_nan(cb)) return nan_pick(a, ca, b, cb);
+    const uint32_t s = ((a.se ^ b.se) >> 15) & 1;
+    if (ca == C_INF || cb == C_INF) {
+        if (ca == C_ZERO || cb == C_ZERO) return defnan();
+        return X80{1ull << 63, (s << 15) | kEmax};
+    }
+    if (ca == C_ZERO || cb == C_ZERO) return X80{0, s << 15};
+    int Ea = (int) (a.se & kEmax), Eb = (int) (b.se & kEmax);
+    Ea = Ea ? Ea : 1;
+    Eb = Eb ? Eb : 1;
+    u128 P = (u128) a.m * (u128) b.m;            // exact, nonzero
+    const int lz = clz128(P);
+    P <<= lz;
+    // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = P * 2^(Ea+Eb-2bias-126-lz)
+    //   = S * 2^(E - bias - 127)  =>  E = Ea + Eb - bias + 1 - lz
+    const int E = Ea + Eb - kBias + 1 - lz;
+    return round_pack(s, E, P);
+}
+
+// fcomi ordering; false when unordered (NaN or unsupported encoding)
+OSGPU_HD inline bool less(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD || is_nan(ca) || is_nan(cb)) return false;
+    const bool za = ca == C_ZERO, zb = cb == C_ZERO;
+    if (za && zb) return false;
+    const bool na = !za && ((a.se >> 15) & 1), nb = !zb && ((b.se >> 15) & 1);
+    if (na != nb) return na;
+    // magnitude keys (E, m): zero < denormal/pseudo-denormal (E=1) < ...
+    uint32_t ea = za ? 0 : ((a.se & kEmax) ? (a.se & kEmax) : 1);
+    uint32_t eb = zb ? 0 : ((b.se & kEmax) ? (b.se & kEmax) : 1);
+    const uint64_t ma = za ? 0 : a.m, mb = zb ? 0 : b.m;
+    const bool mag_lt = ea < eb || (ea == eb && ma < mb);
+    const bool mag_gt = ea > eb || (ea == eb && ma > mb);
+    return na ? mag_gt : mag_lt;
+}
+
+}  // namespace x87
+}  // namespace osgpu

@@ -28,7 +28,7 @@ CTYPE = {
     "double": ctypes.c_double, "longdouble": ctypes.c_longdouble,
     "complexf": ctypes.c_float * 2, "complexd": ctypes.c_double * 2,
 }
-PATH_AUTO, PATH_P2P, PATH_RCCL = 0, 1, 2
+PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
 
 
 def has_op(t: str, op: str) -> bool:

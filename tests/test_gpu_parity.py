@@ -20,8 +20,8 @@ import osgpu
 
 pytestmark = pytest.mark.gpu
 
-# x87 80-bit long double: soft-float kernel not in this build yet
-LD_ON_GPU = False
+# x87 80-bit long double runs on the GPU through the soft-float in x87.hpp
+LD_ON_GPU = True
 CASES = [c for c in O.load_cases() if LD_ON_GPU or c["type"] != "longdouble"]
 
 
@@ -102,9 +102,22 @@ def test_device_resident_matches_golden(torch_cuda, pair, cases):
         check(c, run_case(tm, c))
 
 
+def test_pull_path_matches_golden(torch_cuda):
+    """The same cases forced onto the pull form (every PE reads every source,
+    the reference's own schedule) instead of the owner-computes team kernel."""
+    tm = team(device=True)
+    tm.lib.osgpu_set_path(osgpu.PATH_PULL)
+    try:
+        for c in CASES:
+            if c["nreduce"] <= 4097 and c["npes"] in (2, 3, 8) and c["tag"] != "subset":
+                check(c, run_case(tm, c))
+    finally:
+        tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
+
+
 @pytest.mark.parametrize("t,op", [("double", "sum"), ("float", "prod"), ("int", "xor"),
                                   ("complexd", "prod"), ("short", "min"),
-                                  ("complexf", "sum")])
+                                  ("complexf", "sum"), ("longdouble", "sum")])
 def test_in_place_target_equals_source(torch_cuda, t, op):
     tm = team(device=True)
     for c in CASES:
@@ -115,7 +128,7 @@ def test_in_place_target_equals_source(torch_cuda, t, op):
 
 @pytest.mark.parametrize("t,op", [("int", "sum"), ("double", "sum"), ("long", "and"),
                                   ("float", "min"), ("complexd", "prod"),
-                                  ("short", "prod")])
+                                  ("short", "prod"), ("longdouble", "prod")])
 def test_host_staged_matches_golden(torch_cuda, t, op, monkeypatch):
     monkeypatch.setenv("OSGPU_HOST_CHUNK_BYTES", "4096")  # many chunks
     tm = team(device=False)

@@ -1,0 +1,84 @@
+"""Multi-process (one process per PE) runs of libosgpu_reduce.so, world size 2.
+
+* CPU (gloo, no GPU): PE services supplied through Python callbacks
+  (my_pe = rank, shmem_barrier = dist.barrier) as bench.py does at N > 1;
+  fold orders and shard partitions agree across ranks; the nreduce = 0
+  collective performs exactly the reference's two barriers
+  (src/reductions.c:82,113).
+* GPU: two processes share cuda:0, export/import their device heaps over HIP
+  IPC (the multi-GPU path's mechanism) and run shmem_*_to_all on the team
+  path, the pull path and in place; every PE's target must equal the oracle
+  bit for bit.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "support", "mp_worker.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(mode, world, tmp_path, timeout=600):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, WORKER, mode, str(tmp_path)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+    return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+
+
+def test_host_logic_world2(tmp_path):
+    res = launch("host", 2, tmp_path)
+    assert [r["order"] for r in res] == [O.fold_order(0, 0, 0, 2), O.fold_order(1, 0, 0, 2)]
+    for eb in ("2", "4", "8", "16"):
+        for k, n in enumerate((0, 1, 63, 1000, 4097, 1 << 20)):
+            lo0, hi0 = res[0]["shards"][eb][k]
+            lo1, hi1 = res[1]["shards"][eb][k]
+            assert lo0 == 0 and hi0 == lo1 and hi1 == n
+    assert [r["barriers"] for r in res] == [2, 2]
+
+
+@pytest.mark.gpu
+def test_ipc_heaps_two_processes(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("ipc", 2, tmp_path)
+    specs = (("double", "sum", 100_003, "wide"), ("float", "min", 4097, "edge"),
+             ("int", "prod", 1000, "bits"), ("complexd", "prod", 999, "edge"),
+             ("longdouble", "sum", 517, "wide"), ("short", "xor", 4096, "bits"))
+    for t, op, n, d in specs:
+        src = [O.gen_input(t, n, O.pe_seed(0xABC, r), d) for r in range(2)]
+        want = O.to_all(t, op, src)
+        for r in range(2):
+            wb = O.value_bytes(want[r]).reshape(-1).tobytes().hex()
+            for key, hexv in res[r]["out"].items():
+                if key.startswith(f"{t}/{op}/"):
+                    assert hexv == wb, (key, r)
