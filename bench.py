@@ -13,11 +13,13 @@ N = 1 (default) -- BASELINE config 2: nreduce = 64 Mi doubles, 1 MI355X,
 
 N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   shmem_double_sum_to_all(nreduce = 64 Mi per PE) over all N PEs (weak
-  scaling: per-GPU data fixed).  Path: RCCL allreduce over xGMI (default) or
-  the exact-order peer-read kernel over IPC-mapped heaps (--path p2p).  Per
-  step the job combines N sources into N targets; value counts the same
-  algorithmic bytes as N=1, (N + 1) * nreduce * 8 per PE result summed over
-  the N PEs, divided by the max-over-ranks time.
+  scaling: per-GPU data fixed).  Primary path: the exact owner-computes team
+  kernel over IPC-mapped peer heaps (xGMI), PE services from an intra-node
+  shared-memory runtime (tests/support/pe_shm.c); a sampled bit-exact parity
+  check against the oracle is reported.  RCCL allreduce is timed afterwards
+  as a secondary figure ("rccl").  value = steps * (N + 1) * nreduce * 8 / t
+  (SURVEY.md 8d aggregate: sum over GPUs of the shard-fold bytes), t = the
+  max over ranks.
 
 Also printed (same JSON line): roofline of the dominant kernel from HIP
 events on the launch stream, the reference's CPU loop shape timed on this
@@ -45,7 +47,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--nreduce", type=int, default=64 << 20)
-    ap.add_argument("--path", choices=["rccl", "p2p"], default="rccl")
+    ap.add_argument("--path", choices=["rccl", "p2p"], default="p2p",
+                    help="N>1: primary path is always the exact p2p team kernel; "
+                         "rccl is measured after it unless --no-rccl")
+    ap.add_argument("--no-rccl", action="store_true")
+    ap.add_argument("--rccl-timeout", type=float, default=240.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=64 << 20,
@@ -88,25 +94,36 @@ def cpu_baseline(n):
                        f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
 
 
-def api_call_time(n, reps=10):
-    """Full shmem_double_sum_to_all through the C ABI: 2 threads-as-PEs on
-    cuda:0 (P2P path, barriers + stream syncs included)."""
-    import numpy as np
+def api_call_time(n, reps=20):
+    """Full shmem_double_sum_to_all through the C ABI, timed in C
+    (tests/support/pe_threads.c:pet_time_to_all): a 2-PE active set, one
+    pthread per PE, both PEs' symmetric heaps in this GPU's HBM.  Includes
+    the entry device sync, the two barriers and the stream syncs.  Team path
+    (owner-computes, both PEs' kernels: 2*2*n*8 HBM bytes per collective)
+    and pull path (each PE folds both sources: 2*3*n*8)."""
+    import osgpu
     from support import team as T
     tm = T.Team(2, 2 * n * 8 + 8192, device=True)
     toff = (n * 8 + 4095) // 4096 * 4096
+    import torch
     for pe in range(2):
-        tm.buf[pe * tm.H: pe * tm.H + n * 8].view(__import__("torch").float64).uniform_(1, 2)
-    tm.run("double", "sum", toff, 0, n)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        tm.run("double", "sum", toff, 0, n)
-        ts.append(time.perf_counter() - t0)
-    ts.sort()
-    med = ts[len(ts) // 2]
-    return {"ms_per_call": med * 1e3, "GiB_s": 2 * 3 * n * 8 / med / GIB,
-            "note": "2 PEs (threads) on one GPU, both PEs' calls, barrier-to-barrier"}
+        tm.buf[pe * tm.H: pe * tm.H + n * 8].view(torch.float64).uniform_(1, 2)
+    torch.cuda.synchronize()
+    fn = ctypes.cast(tm.lib.shmem_double_sum_to_all, ctypes.c_void_p)
+    tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
+    src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
+    tm.pet.pet_time_to_all.restype = ctypes.c_double
+    tm.pet.pet_time_to_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    out = {"note": "2 PEs (pthreads) on one GPU; one collective call, start barrier "
+                   "to PE 0's return, median of %d" % reps}
+    for name, path, hbm in (("team", osgpu.PATH_AUTO, 4), ("pull", osgpu.PATH_PULL, 6)):
+        tm.lib.osgpu_set_path(path)
+        sec = tm.pet.pet_time_to_all(fn, 2, tgt, src, n, reps)
+        out[name] = {"ms_per_call": sec * 1e3, "hbm_GBs": hbm * n * 8 / sec / 1e9,
+                     "combine_GiBs_2PE": 2 * 3 * n * 8 / sec / GIB}
+    tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
+    return out
 
 
 def bench_single(args):
@@ -185,63 +202,72 @@ def bench_single(args):
     print(json.dumps(res), flush=True)
 
 
+def _sample_parity(L, rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15):
+    """Bit-exact check of this PE's target on a sample of elements: every
+    rank contributes its source at the sampled indices (gloo), the oracle
+    folds them in this PE's order (src/reductions.c:79-111)."""
+    import numpy as np
+    import torch
+    import oracle as O
+    g = torch.Generator().manual_seed(1234)
+    idx = torch.randint(0, n, (nsamp,), generator=g)
+    mine = src[idx.to(src.device)].cpu()
+    allv = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    srcs = [a.numpy() for a in allv]
+    want = O.fold_with(O.op_elementwise, "double", fn_op, srcs, rank, 0, 0, world)
+    got = tgt[idx.to(tgt.device)].cpu().numpy()
+    bad = int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))
+    rel = float(np.max(np.abs(got - want) / np.abs(want))) if nsamp else 0.0
+    return {"checked": nsamp, "bit_mismatches": bad, "max_rel_err": rel}
+
+
+def _timed(step, steps, warmup, dist, torch):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    tt = torch.tensor([t], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
 def bench_multi(args):
+    """One PE per GPU (torchrun).  Primary: the exact owner-computes team
+    kernel over IPC-mapped peer heaps (xGMI).  Secondary: RCCL allreduce,
+    run after the primary result is safe (a watchdog prints the line if it
+    stalls)."""
+    import threading
     import torch
     import torch.distributed as dist
     import osgpu
+    from support import peshm
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev_id = local % max(ndev, 1)
+    torch.cuda.set_device(dev_id)
     dist.init_process_group("gloo")
     L = osgpu.load()
+    PES = peshm.init(rank, world, 1 << 20, dist, tag="b")
+    assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
     n = args.nreduce
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", dev_id)
 
-    @ctypes.CFUNCTYPE(ctypes.c_int)
-    def my_pe():
-        return rank
-
-    @ctypes.CFUNCTYPE(ctypes.c_int)
-    def n_pes():
-        return world
-
-    @ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                      ctypes.POINTER(ctypes.c_long))
-    def barrier(a, b, c, p):
-        dist.barrier()
-
-    ops = osgpu.PeOps(my_pe, n_pes, barrier,
-                      ctypes.cast(None, osgpu.PeOps._fields_[3][1]))
-    assert L.osgpu_set_pe_ops(ctypes.byref(ops)) == 0
-
-    heap = torch.empty(2 * n * 8 + 4096, dtype=torch.uint8, device=dev)
+    off_t = (n * 8 + 4095) // 4096 * 4096
+    H = off_t + n * 8
+    heap = torch.empty(H, dtype=torch.uint8, device=dev)
     src = heap[: n * 8].view(torch.float64)
-    tgt = heap[n * 8 + 4096: n * 8 + 4096 + n * 8].view(torch.float64)
-    src.uniform_(1.0, 2.0)
-    if args.path == "rccl":
-        uid = (ctypes.c_char * 128)()
-        if rank == 0:
-            assert L.osgpu_rccl_unique_id(uid) == 0
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (ctypes.c_char * 128).from_buffer_copy(obj[0])
-        assert L.osgpu_rccl_init(world, rank, uid) == 0
-        L.osgpu_set_path(osgpu.PATH_RCCL)
-    else:
-        h = (ctypes.c_char * 64)()
-        assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
-        hs = [None] * world
-        dist.all_gather_object(hs, bytes(h))
-        for pe in range(world):
-            if pe == rank:
-                base = heap.data_ptr()
-            else:
-                hb = (ctypes.c_char * 64).from_buffer_copy(hs[pe])
-                base = L.osgpu_ipc_open(hb)
-                assert base, L.osgpu_last_error().decode()
-            assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), heap.numel()) == 0
-        L.osgpu_set_path(osgpu.PATH_P2P)
+    tgt = heap[off_t: off_t + n * 8].view(torch.float64)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    src.uniform_(1.0, 2.0, generator=g)
+    torch.cuda.synchronize()
     psync = (ctypes.c_long * 128)()
     wrk = (ctypes.c_double * 64)()
     fn = L.shmem_double_sum_to_all
@@ -249,41 +275,90 @@ def bench_multi(args):
     def step():
         fn(tgt.data_ptr(), src.data_ptr(), n, 0, 0, world, wrk, psync)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    # ---- primary: exact team kernel over IPC-mapped heaps
+    h = (ctypes.c_char * 64)()
+    assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
+    hs = [None] * world
+    dist.all_gather_object(hs, bytes(h))
+    mapped = []
+    for pe in range(world):
+        if pe == rank:
+            base = heap.data_ptr()
+        else:
+            base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(hs[pe]))
+            assert base, L.osgpu_last_error().decode()
+            mapped.append(base)
+        assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), H) == 0
+    L.osgpu_set_path(osgpu.PATH_P2P)
+    t = _timed(step, args.steps, args.warmup, dist, torch)
+    parity = _sample_parity(L, rank, world, src, tgt, n, "sum", dist)
+    pars = [None] * world
+    dist.all_gather_object(pars, parity)
+    B = (world + 1) * n * 8          # sum over GPUs of shard-fold bytes
+    res = {
+        "metric": "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2/4/8 GPU",
+        "value": args.steps * B / t / GIB,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: uniform [1,2) doubles resident in HBM",
+        "config": {"workload": f"shmem_double_sum_to_all over {world} PEs, one per MI355X, "
+                               f"nreduce={n} per PE, exact owner-computes team kernel over "
+                               f"IPC-mapped peer HBM (xGMI)",
+                   "nreduce": n, "path": "p2p-team", "bytes_per_step": B,
+                   "bytes_convention": "(P+1)*nreduce*8 per step (SURVEY.md 8d aggregate)",
+                   "algbw_GiBs": n * 8 * args.steps / t / GIB,
+                   "parallelism": f"pe{world}"},
+        "parity_sample": {"checked_per_pe": parity["checked"],
+                          "bit_mismatches": sum(p["bit_mismatches"] for p in pars)},
+    }
+    out = {"res": res}
+    printed = threading.Event()
+
+    def emit():
+        if rank == 0 and not printed.is_set():
+            printed.set()
+            print(json.dumps(out["res"]), flush=True)
+
+    # ---- secondary: RCCL allreduce (guarded)
+    if args.path == "rccl" or not args.no_rccl:
+        def watchdog():
+            if not done.wait(args.rccl_timeout):
+                emit()
+                os._exit(0)
+        done = threading.Event()
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            uid = (ctypes.c_char * 128)()
+            if rank == 0:
+                assert L.osgpu_rccl_unique_id(uid) == 0
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=0)
+            rc = L.osgpu_rccl_init(world, rank, (ctypes.c_char * 128).from_buffer_copy(obj[0]))
+            if rc != 0:
+                raise RuntimeError(L.osgpu_last_error().decode())
+            L.osgpu_set_path(osgpu.PATH_RCCL)
+            t2 = _timed(step, args.steps, args.warmup, dist, torch)
+            p2 = _sample_parity(L, rank, world, src, tgt, n, "sum", dist)
+            pars2 = [None] * world
+            dist.all_gather_object(pars2, p2)
+            res["rccl"] = {"value": args.steps * B / t2 / GIB, "ms_per_step": t2 / args.steps * 1e3,
+                           "bit_mismatches_vs_reference_order": sum(p["bit_mismatches"] for p in pars2),
+                           "max_rel_err": max(p["max_rel_err"] for p in pars2)}
+        except Exception as e:  # reported, never hidden
+            res["rccl"] = {"error": repr(e)[:300]}
+        done.set()
+    emit()
+    L.osgpu_set_path(osgpu.PATH_AUTO)
     dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    tt = torch.tensor([t], dtype=torch.float64)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t = float(tt.item())
-    B = world * (world + 1) * n * 8
-    if rank == 0:
-        res = {
-            "metric": "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2/4/8 GPU",
-            "value": args.steps * B / t / GIB,
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": t / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: uniform [1,2) doubles resident in HBM",
-            "config": {"workload": f"shmem_double_sum_to_all over {world} PEs, one per "
-                                   f"MI355X, nreduce=64Mi per PE ({args.path} path)",
-                       "nreduce": n, "path": args.path,
-                       "bytes_per_step": B,
-                       "parallelism": f"pe{world}"},
-        }
-        print(json.dumps(res), flush=True)
-    dist.barrier()
+    for p in mapped:
+        L.osgpu_ipc_close(ctypes.c_void_p(p))
     dist.destroy_process_group()
 
 

@@ -55,9 +55,37 @@ def main():
     dist.init_process_group("gloo")
     L = osgpu.load()
     counter = [0]
-    ops, keep = pe_ops(rank, world, counter)
-    assert L.osgpu_set_pe_ops(ctypes.byref(ops)) == 0
+    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode == "hoststaged":
+        from support import peshm
+        PES = peshm.init(rank, world, 1 << 24, dist)
+        assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
+    else:
+        ops, keep = pe_ops(rank, world, counter)
+        assert L.osgpu_set_pe_ops(ctypes.byref(ops)) == 0
     res = {"rank": rank}
+    if mode == "hoststaged":
+        import oracle as O
+        base = PES.pes_heap(rank)
+        out = {}
+        for t, op, n, dist_ in (("double", "sum", 300_007, "wide"), ("float", "max", 4097, "edge"),
+                                ("long", "or", 65, "or"), ("complexf", "prod", 1000, "edge"),
+                                ("longdouble", "min", 333, "edge")):
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            src = np.ascontiguousarray(O.gen_input(t, n, O.pe_seed(0xDEF, rank), dist_))
+            raw = src.view(np.uint8).reshape(-1)
+            toff = (n * s + 4095) // 4096 * 4096
+            for inplace in (False, True):
+                ctypes.memmove(base, raw.ctypes.data, raw.size)
+                tgt = base + (0 if inplace else toff)
+                psync = (ctypes.c_long * 128)()
+                wrk = (ctypes.c_byte * 4096)()
+                getattr(L, f"shmem_{t}_{op}_to_all")(tgt, base, n, 0, 0, world, wrk, psync)
+                got = np.frombuffer(ctypes.string_at(tgt, n * s), dtype=np.uint8)
+                if t == "longdouble":
+                    got = got.reshape(-1, 16)[:, :10].reshape(-1)
+                out[f"{t}/{op}/host/{int(inplace)}"] = got.tobytes().hex()
+                dist.barrier()
+        res["out"] = out
     if mode == "host":
         res["order"] = osgpu.fold_order(rank, 0, 0, world)
         res["shards"] = {str(eb): [osgpu.shard_range(n, world, rank, eb)

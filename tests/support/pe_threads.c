@@ -115,4 +115,67 @@ void pet_getmem(void *dest, const void *src, size_t n, int pe)
 
 static pe_ops_t g_table = {pet_my_pe, pet_n_pes, pet_barrier, pet_getmem};
 
+/* ---- C-level timing of the API: npes pthreads each call fn (a
+   shmem_<T>_<op>_to_all) `reps` times; PE 0 times each collective call from
+   a common start (pthread barrier) to its own return, after one warm-up. */
+typedef void (*to_all_fn)(void *, void *, int, int, int, int, void *, long *);
+
+typedef struct {
+    to_all_fn fn;
+    int npes, n, reps, me;
+    void **tgt, **src;
+    pthread_barrier_t *bar;
+    double *times;
+} timing_arg;
+
+#include <time.h>
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+static void *timing_body(void *p)
+{
+    timing_arg *a = (timing_arg *) p;
+    long psync[128] = {0};
+    char wrk[4096];
+    t_me = a->me;
+    for (int r = 0; r <= a->reps; r++) {
+        pthread_barrier_wait(a->bar);
+        double t0 = now_s();
+        a->fn(a->tgt[a->me], a->src[a->me], a->n, 0, 0, a->npes, wrk, psync);
+        pthread_barrier_wait(a->bar);
+        if (a->me == 0) a->times[r] = now_s() - t0;
+    }
+    return NULL;
+}
+
+static int cmpd(const void *x, const void *y)
+{
+    double a = *(const double *) x, b = *(const double *) y;
+    return a < b ? -1 : a > b;
+}
+
+double pet_time_to_all(void *fn, int npes, void **tgt, void **src, int n, int reps)
+{
+    if (npes < 1 || npes > MAXPE || reps < 1) return -1.0;
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned) npes);
+    double *times = calloc((size_t) reps + 1, sizeof(double));
+    pthread_t th[MAXPE];
+    timing_arg args[MAXPE];
+    for (int i = 0; i < npes; i++) {
+        args[i] = (timing_arg){(to_all_fn) fn, npes, n, reps, i, tgt, src, &bar, times};
+        pthread_create(&th[i], NULL, timing_body, &args[i]);
+    }
+    for (int i = 0; i < npes; i++) pthread_join(th[i], NULL);
+    pthread_barrier_destroy(&bar);
+    qsort(times + 1, (size_t) reps, sizeof(double), cmpd);
+    double med = times[1 + reps / 2];
+    free(times);
+    return med;
+}
+
 const void *pet_ops(void) { return &g_table; }

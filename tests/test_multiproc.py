@@ -65,20 +65,43 @@ def test_host_logic_world2(tmp_path):
     assert [r["barriers"] for r in res] == [2, 2]
 
 
+def _check_specs(res, specs, seed):
+    for t, op, n, d in specs:
+        src = [O.gen_input(t, n, O.pe_seed(seed, r), d) for r in range(len(res))]
+        want = O.to_all(t, op, src)
+        for r in range(len(res)):
+            wb = O.value_bytes(want[r]).reshape(-1).tobytes().hex()
+            keys = [k for k in res[r]["out"] if k.startswith(f"{t}/{op}/")]
+            assert keys
+            for key in keys:
+                assert res[r]["out"][key] == wb, (key, r)
+
+
 @pytest.mark.gpu
-def test_ipc_heaps_two_processes(tmp_path):
+@pytest.mark.parametrize("pes", ["gloo", "shm"])
+def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("OSGPU_TEST_PES", pes)
     res = launch("ipc", 2, tmp_path)
     specs = (("double", "sum", 100_003, "wide"), ("float", "min", 4097, "edge"),
              ("int", "prod", 1000, "bits"), ("complexd", "prod", 999, "edge"),
              ("longdouble", "sum", 517, "wide"), ("short", "xor", 4096, "bits"))
-    for t, op, n, d in specs:
-        src = [O.gen_input(t, n, O.pe_seed(0xABC, r), d) for r in range(2)]
-        want = O.to_all(t, op, src)
-        for r in range(2):
-            wb = O.value_bytes(want[r]).reshape(-1).tobytes().hex()
-            for key, hexv in res[r]["out"].items():
-                if key.startswith(f"{t}/{op}/"):
-                    assert hexv == wb, (key, r)
+    _check_specs(res, specs, 0xABC)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_staged_processes(tmp_path, world):
+    """Host symmetric heaps (shared memory), getmem between processes, the
+    combine on the GPU: the reference's own data placement."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("hoststaged", world, tmp_path)
+    specs = (("double", "sum", 300_007, "wide"), ("float", "max", 4097, "edge"),
+             ("long", "or", 65, "or"), ("complexf", "prod", 1000, "edge"),
+             ("longdouble", "min", 333, "edge"))
+    _check_specs(res, specs, 0xDEF)
+
