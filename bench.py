@@ -94,6 +94,54 @@ def cpu_baseline(n):
                        f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
 
 
+def _timer_sig(pet):
+    pet.pet_time_to_all.restype = ctypes.c_double
+    pet.pet_time_to_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_int]
+
+
+def host_staged_time(n, reps=5):
+    """The reference's data placement: sources and targets in HOST symmetric
+    heaps.  shmem_double_sum_to_all over a 2-PE set on one GPU (pthreads as
+    PEs), STAGED path: H2D own source -> team exchange on the GPU -> D2H,
+    pipelined in 32 MiB chunks.  Timed in C, pinned heap (osgpu_host_register)
+    and pageable heap.  Both PEs share this GPU's one PCIe link, so per call
+    2*n*8 bytes go H2D and 2*n*8 D2H."""
+    import osgpu
+    from support import team as T
+    L = osgpu.load()
+    L.osgpu_finalize()
+    out = {"note": f"2 PEs (pthreads) on one GPU, host heaps, nreduce={n} doubles per PE; "
+                   f"PCIe bytes per call = 2*{n}*8 H2D + 2*{n}*8 D2H"}
+    for pinned in (True, False):
+        tm = T.Team(2, 2 * n * 8 + 8192, device=False)
+        toff = (n * 8 + 4095) // 4096 * 4096
+        import numpy as np
+        for pe in range(2):
+            lo = tm.hoff + pe * tm.H
+            tm.hbuf[lo:lo + n * 8].view(np.float64)[:] = 1.5 + pe
+        if pinned:
+            assert L.osgpu_host_register(ctypes.c_void_p(tm.base), 2 * tm.H) == 0
+        fn = ctypes.cast(L.shmem_double_sum_to_all, ctypes.c_void_p)
+        tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
+        src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
+        ps = (ctypes.c_void_p * 2)(tm.ptr(0, tm.psync_off), tm.ptr(1, tm.psync_off))
+        _timer_sig(tm.pet)
+        sec = tm.pet.pet_time_to_all(fn, 2, tgt, src, ps, n, reps)
+        ok = bool((tm.hbuf[tm.hoff + toff: tm.hoff + toff + n * 8].view(np.float64) == 4.0).all())
+        out["pinned" if pinned else "pageable"] = {
+            "ms_per_call": sec * 1e3,
+            "pcie_GBs_each_way": 2 * n * 8 / sec / 1e9,
+            "algbw_GiBs_per_PE": n * 8 / sec / GIB,
+            "correct": ok}
+        if pinned:
+            L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
+        L.osgpu_finalize()
+        del tm
+    return out
+
+
 def api_call_time(n, reps=20):
     """Full shmem_double_sum_to_all through the C ABI, timed in C
     (tests/support/pe_threads.c:pet_time_to_all): a 2-PE active set, one
@@ -112,14 +160,12 @@ def api_call_time(n, reps=20):
     fn = ctypes.cast(tm.lib.shmem_double_sum_to_all, ctypes.c_void_p)
     tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
     src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
-    tm.pet.pet_time_to_all.restype = ctypes.c_double
-    tm.pet.pet_time_to_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    _timer_sig(tm.pet)
     out = {"note": "2 PEs (pthreads) on one GPU; one collective call, start barrier "
                    "to PE 0's return, median of %d" % reps}
     for name, path, hbm in (("team", osgpu.PATH_AUTO, 4), ("pull", osgpu.PATH_PULL, 6)):
         tm.lib.osgpu_set_path(path)
-        sec = tm.pet.pet_time_to_all(fn, 2, tgt, src, n, reps)
+        sec = tm.pet.pet_time_to_all(fn, 2, tgt, src, None, n, reps)
         out[name] = {"ms_per_call": sec * 1e3, "hbm_GBs": hbm * n * 8 / sec / 1e9,
                      "combine_GiBs_2PE": 2 * 3 * n * 8 / sec / GIB}
     tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
@@ -197,6 +243,10 @@ def bench_single(args):
             res["api"] = api_call_time(n)
         except Exception as e:  # report, never hide
             res["api"] = {"error": repr(e)}
+        try:
+            res["host_staged"] = host_staged_time(n)
+        except Exception as e:
+            res["host_staged"] = {"error": repr(e)}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_n)
     print(json.dumps(res), flush=True)

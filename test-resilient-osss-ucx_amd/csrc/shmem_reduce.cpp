@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <map>
 #include <mutex>
@@ -168,18 +169,29 @@ int path_mode()
     return g_path;
 }
 
-// -------------------------------------------------------- per-thread state
+// ------------------------------------------------------ per-PE / per-thread
 
-struct ThreadCtx {
-    int device = -1;
+// Resources of one PE on one device (stream, scratch, pinned staging).  Keyed
+// by (PE, device), not by thread: a PE is one logical thread of execution
+// whatever OS thread happens to make its calls, so nothing leaks when a
+// runtime runs PEs on short-lived threads.  Calls of one PE never overlap.
+struct PeCtx {
     hipStream_t stream = nullptr;
-    bool user_stream = false;
     void *dscratch = nullptr;
     size_t dscratch_bytes = 0;
     void *hstage = nullptr;  // pinned
     size_t hstage_bytes = 0;
 };
-thread_local ThreadCtx t_ctx;
+std::map<std::pair<int, int>, PeCtx *> g_pectx;
+
+// per-thread: the stream chosen with osgpu_set_stream (overrides the PE's),
+// and a default stream for the raw osgpu_combine launcher
+struct ThreadStream {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    bool user_stream = false;
+};
+thread_local ThreadStream t_ctx;
 
 hipStream_t thread_stream(const char *where)
 {
@@ -192,28 +204,49 @@ hipStream_t thread_stream(const char *where)
     return t_ctx.stream;
 }
 
-void *device_scratch(const char *where, size_t bytes)
+PeCtx &pe_ctx(const char *where, int me)
 {
-    if (t_ctx.dscratch_bytes < bytes) {
-        if (t_ctx.dscratch) HIPCHK(where, hipFree(t_ctx.dscratch));
-        t_ctx.dscratch = nullptr;
-        t_ctx.dscratch_bytes = 0;
-        HIPCHK(where, hipMalloc(&t_ctx.dscratch, bytes));
-        t_ctx.dscratch_bytes = bytes;
+    int dev = 0;
+    HIPCHK(where, hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_mu);
+    PeCtx *&p = g_pectx[std::make_pair(me, dev)];
+    if (!p) {
+        p = new PeCtx();
+        HIPCHK(where, hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     }
-    return t_ctx.dscratch;
+    return *p;
 }
 
-void *host_stage(const char *where, size_t bytes)
+hipStream_t pe_stream(const char *where, int me)
 {
-    if (t_ctx.hstage_bytes < bytes) {
-        if (t_ctx.hstage) HIPCHK(where, hipHostFree(t_ctx.hstage));
-        t_ctx.hstage = nullptr;
-        t_ctx.hstage_bytes = 0;
-        HIPCHK(where, hipHostMalloc(&t_ctx.hstage, bytes, hipHostMallocDefault));
-        t_ctx.hstage_bytes = bytes;
+    if (t_ctx.user_stream && t_ctx.stream) return t_ctx.stream;
+    return pe_ctx(where, me).stream;
+}
+
+void *device_scratch(const char *where, int me, size_t bytes)
+{
+    PeCtx &x = pe_ctx(where, me);
+    if (x.dscratch_bytes < bytes) {
+        if (x.dscratch) HIPCHK(where, hipFree(x.dscratch));
+        x.dscratch = nullptr;
+        x.dscratch_bytes = 0;
+        HIPCHK(where, hipMalloc(&x.dscratch, bytes));
+        x.dscratch_bytes = bytes;
     }
-    return t_ctx.hstage;
+    return x.dscratch;
+}
+
+void *host_stage(const char *where, int me, size_t bytes)
+{
+    PeCtx &x = pe_ctx(where, me);
+    if (x.hstage_bytes < bytes) {
+        if (x.hstage) HIPCHK(where, hipHostFree(x.hstage));
+        x.hstage = nullptr;
+        x.hstage_bytes = 0;
+        HIPCHK(where, hipHostMalloc(&x.hstage, bytes, hipHostMallocDefault));
+        x.hstage_bytes = bytes;
+    }
+    return x.hstage;
 }
 
 enum MemKind { MEM_HOST = 0, MEM_DEVICE = 1 };
@@ -317,7 +350,7 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
 void run_team(const Call &c, const std::vector<const void *> &srcs,
               const std::vector<void *> &dsts, int idx)
 {
-    hipStream_t st = thread_stream(c.name);
+    hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
     long long lo = 0, hi = 0;
     osgpu_shard_range(c.nreduce, c.PE_size, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
@@ -340,12 +373,12 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
 
 void run_p2p(const Call &c, const std::vector<const void *> &srcs)
 {
-    hipStream_t st = thread_stream(c.name);
+    hipStream_t st = pe_stream(c.name, c.me);
     // prior device work of this process that produced `source` must be done
     HIPCHK(c.name, hipDeviceSynchronize());
     barrier(c);  // src/reductions.c:82 -- every source is ready
     const bool overlap = c.PE_size > 1 && ranges_overlap(c.target, c.source, c.nbytes);
-    void *out = overlap ? device_scratch(c.name, c.nbytes) : c.target;
+    void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
     hipError_t e = osgpu::launch_combine(c.type, c.op, out, srcs.data(), c.PE_size,
                                          (size_t) c.nreduce, st);
     if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
@@ -396,10 +429,10 @@ void run_rccl(const Call &c)
     ncclRedOp_t rop;
     size_t mult;
     rccl_types(c.type, c.op, &dt, &rop, &mult);
-    hipStream_t st = thread_stream(c.name);
+    hipStream_t st = pe_stream(c.name, c.me);
     HIPCHK(c.name, hipDeviceSynchronize());
     const bool overlap = ranges_overlap(c.target, c.source, c.nbytes) && c.target != c.source;
-    void *out = overlap ? device_scratch(c.name, c.nbytes) : c.target;
+    void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
     ncclResult_t r = ncclAllReduce(c.source, out, (size_t) c.nreduce * mult, dt, rop,
                                    g_rccl.world, st);
     if (r != ncclSuccess) fatal(c.name, "ncclAllReduce: %s", ncclGetErrorString(r));
@@ -407,6 +440,188 @@ void run_rccl(const Call &c)
     if (overlap) {
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
         HIPCHK(c.name, hipStreamSynchronize(st));
+    }
+}
+
+// ---------------------------------------------------------------------
+// STAGED host path: H2D of my own source -> exchange ON THE GPUs (team
+// kernel over every PE's device staging buffers, IPC-mapped) -> D2H.
+// Pipelined over chunks with two slots and three streams:
+//   H2D(c+1) || team(c) || D2H(c-1).
+// The peers' data never crosses the host: PCIe carries N*s in and N*s out
+// per PE, xGMI carries the exchange.  Setup (once per active set) publishes
+// each PE's staging allocation through spare words of the symmetric pSync
+// (the reference's barrier only uses pSync[0], src/shmemc/barrier.c:64-97)
+// and reads the peers' with shmem_getmem; pSync is returned zeroed.
+// ---------------------------------------------------------------------
+
+constexpr int kPsyncBase = 16;  // pSync[16..28] used during setup only
+
+struct StageSet {
+    bool ok = false;
+    int device = -1;
+    size_t slot = 0;                 // bytes per slot (in0, in1, out0, out1)
+    char *local = nullptr;
+    std::vector<char *> peer;        // by active-set index
+    std::vector<void *> opened;      // IPC mappings to close
+    hipStream_t st_in = nullptr, st_c = nullptr, st_out = nullptr;
+    hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+    char *in(int i, int s) const { return peer[i] + (size_t) s * slot; }
+    char *out(int i, int s) const { return peer[i] + (size_t) (2 + s) * slot; }
+};
+
+std::map<std::tuple<int, int, int, int, int>, StageSet> g_stage;  // (me, set, device)
+
+size_t stage_slot_bytes()
+{
+    const char *e = getenv("OSGPU_STAGE_BYTES");
+    size_t b = e ? strtoull(e, nullptr, 0) : 0;
+    b = b ? b : (size_t) 32 << 20;
+    return (b + 255) & ~(size_t) 255;
+}
+
+struct StageMsg {  // what a PE publishes in pSync[16..28]
+    long handle[OSGPU_IPC_HANDLE_BYTES / sizeof(long)];
+    long raw_ptr, pid, slot, status, pad[3];
+};
+static_assert(sizeof(StageMsg) <= (128 - kPsyncBase) * sizeof(long), "pSync room");
+
+StageSet *stage_setup(const Call &c)
+{
+    int dev = 0;
+    HIPCHK(c.name, hipGetDevice(&dev));
+    auto key = std::make_tuple(c.me, c.PE_start, c.step, c.PE_size, dev);
+    std::unique_lock<std::mutex> lk(g_mu);
+    auto it = g_stage.find(key);
+    if (it != g_stage.end()) return it->second.ok ? &it->second : nullptr;
+    StageSet &S = g_stage[key];  // std::map: the reference stays valid
+    lk.unlock();
+    S.device = dev;
+    S.slot = stage_slot_bytes();
+    HIPCHK(c.name, hipMalloc((void **) &S.local, 4 * S.slot));
+    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_in, hipStreamNonBlocking));
+    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_c, hipStreamNonBlocking));
+    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_out, hipStreamNonBlocking));
+    for (int s = 0; s < 2; s++) {
+        HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_in[s], hipEventDisableTiming));
+        HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_out[s], hipEventDisableTiming));
+    }
+    StageMsg *mine = reinterpret_cast<StageMsg *>(c.pSync + kPsyncBase);
+    memset(mine, 0, sizeof(*mine));
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, S.local) == hipSuccess) memcpy(mine->handle, &h, sizeof(h));
+    else (void) hipGetLastError();
+    mine->raw_ptr = (long) (uintptr_t) S.local;
+    mine->pid = (long) getpid();
+    mine->slot = (long) S.slot;
+    barrier(c);
+    bool ok = true;
+    S.peer.assign(c.PE_size, nullptr);
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        if (pe == c.me) {
+            S.peer[i] = S.local;
+            continue;
+        }
+        StageMsg m;
+        c.ops.getmem(&m, mine, sizeof(m), pe);
+        if ((size_t) m.slot != S.slot) {
+            ok = false;
+        } else if (m.pid == (long) getpid()) {
+            S.peer[i] = (char *) (uintptr_t) m.raw_ptr;   // same process (threads as PEs)
+        } else {
+            hipIpcMemHandle_t ph;
+            memcpy(&ph, m.handle, sizeof(ph));
+            void *p = nullptr;
+            if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
+                S.peer[i] = (char *) p;
+                S.opened.push_back(p);
+            } else {
+                (void) hipGetLastError();
+                ok = false;
+            }
+        }
+    }
+    mine->status = ok ? 1 : 2;
+    barrier(c);
+    bool all_ok = ok;
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        if (pe == c.me) continue;
+        long st = 0;
+        c.ops.getmem(&st, &mine->status, sizeof(long), pe);
+        all_ok = all_ok && st == 1;
+    }
+    barrier(c);
+    memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
+    S.ok = all_ok;
+    return S.ok ? &S : nullptr;
+}
+
+void run_staged(const Call &c, StageSet &S)
+{
+    const size_t s = type_size(c.type);
+    const size_t C = S.slot / s;                       // elements per chunk
+    const size_t N = (size_t) c.nreduce;
+    const size_t nchunks = (N + C - 1) / C;
+    const int P = c.PE_size;
+    int idx = 0;
+    for (int i = 0, pe = c.PE_start; i < P; i++, pe += c.step)
+        if (pe == c.me) idx = i;
+    const bool overlap = ranges_overlap(c.target, c.source, c.nbytes) && c.target != c.source;
+    char *result = overlap ? (char *) malloc(c.nbytes) : (char *) c.target;
+    if (!result) fatal(c.name, "out of memory for the temporary target");
+    const char *src = (const char *) c.source;
+    std::vector<const void *> sp(P);
+    std::vector<void *> dp(P);
+
+    auto h2d = [&](size_t ch) {
+        const size_t n = (ch + 1) * C <= N ? C : N - ch * C;
+        HIPCHK(c.name, hipMemcpyAsync(S.in(idx, ch & 1), src + ch * C * s, n * s,
+                                      hipMemcpyHostToDevice, S.st_in));
+        HIPCHK(c.name, hipEventRecord(S.ev_in[ch & 1], S.st_in));
+    };
+    HIPCHK(c.name, hipDeviceSynchronize());
+    h2d(0);
+    for (size_t ch = 0; ch < nchunks; ch++) {
+        const int sl = (int) (ch & 1);
+        const size_t n = (ch + 1) * C <= N ? C : N - ch * C;
+        if (ch + 1 < nchunks) h2d(ch + 1);   // slot reuse is safe: team(ch-1) ended everywhere
+        HIPCHK(c.name, hipEventSynchronize(S.ev_in[sl]));
+        if (ch >= 2) HIPCHK(c.name, hipEventSynchronize(S.ev_out[sl]));  // my out slot drained
+        barrier(c);  // chunk ch staged on every PE, every out[sl] free
+        if (P == 1) {
+            const void *one = S.in(0, sl);
+            hipError_t e = osgpu::launch_combine(c.type, c.op, S.out(0, sl), &one, 1, n, S.st_c);
+            if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
+        } else if (P <= osgpu::kMaxTeam) {
+            long long lo = 0, hi = 0;
+            osgpu_shard_range((long long) n, P, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
+            for (int i = 0; i < P; i++) {
+                sp[i] = S.in(i, sl) + (size_t) lo * s;
+                dp[i] = S.out(i, sl) + (size_t) lo * s;
+            }
+            if (hi > lo) {
+                hipError_t e = osgpu::launch_team(c.type, c.op, P, dp.data(), sp.data(),
+                                                  (size_t) (hi - lo), S.st_c);
+                if (e != hipSuccess) fatal(c.name, "team launch: %s", hipGetErrorString(e));
+            }
+        } else {  // large active sets: every PE folds its own chunk (pull form)
+            std::vector<int> order(P);
+            fold_order(c.me, c.PE_start, c.step, P, order.data());
+            for (int k = 0; k < P; k++) sp[k] = S.in((order[k] - c.PE_start) / c.step, sl);
+            hipError_t e = osgpu::launch_combine(c.type, c.op, S.out(idx, sl), sp.data(), P, n,
+                                                 S.st_c);
+            if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
+        }
+        HIPCHK(c.name, hipStreamSynchronize(S.st_c));
+        barrier(c);  // every shard of my out[sl] written
+        HIPCHK(c.name, hipMemcpyAsync(result + ch * C * s, S.out(idx, sl), n * s,
+                                      hipMemcpyDeviceToHost, S.st_out));
+        HIPCHK(c.name, hipEventRecord(S.ev_out[sl], S.st_out));
+    }
+    HIPCHK(c.name, hipStreamSynchronize(S.st_out));
+    if (overlap) {
+        memcpy(c.target, result, c.nbytes);
+        free(result);
     }
 }
 
@@ -427,7 +642,7 @@ void run_host(const Call &c)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         fatal(c.name, "no GPU visible: the combine runs only on the GPU");
-    hipStream_t st = thread_stream(c.name);
+    hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
     const int P = c.PE_size;
     std::vector<int> order(P);
@@ -439,8 +654,8 @@ void run_host(const Call &c)
     chunk = (chunk + 1) & ~(size_t) 1;
     const size_t cb = chunk * s;
     // device: P input slots + 1 output slot; pinned: P input slots + output
-    char *dbuf = (char *) device_scratch(c.name, cb * (P + 1));
-    char *hbuf = (char *) host_stage(c.name, cb * (P + 1));
+    char *dbuf = (char *) device_scratch(c.name, c.me, cb * (P + 1));
+    char *hbuf = (char *) host_stage(c.name, c.me, cb * (P + 1));
     const bool overlap = P > 1 && ranges_overlap(c.target, c.source, c.nbytes);
     char *result = overlap ? (char *) malloc(c.nbytes) : (char *) c.target;
     if (!result) fatal(c.name, "out of memory for the temporary target");
@@ -509,7 +724,15 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     if (kt != ks)
         fatal(name, "target and source must both be device or both be host memory");
     if (kt == MEM_HOST) {
-        run_host(c);
+        const char *hp = getenv("OSGPU_HOST_PATH");
+        const bool getmem_only = hp && !strcmp(hp, "getmem");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+            fatal(name, "no GPU visible: the combine runs only on the GPU");
+        if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
+        StageSet *S = getmem_only ? nullptr : stage_setup(c);
+        if (S) run_staged(c, *S);
+        else run_host(c);
         return;
     }
     int cur = 0;
@@ -723,6 +946,54 @@ int osgpu_rccl_finalize(void)
     ncclResult_t r = ncclCommDestroy(g_rccl.world);
     g_rccl = Rccl();
     return r == ncclSuccess ? OSGPU_OK : OSGPU_ERCCL;
+}
+
+int osgpu_finalize(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &kv : g_stage) {
+        StageSet &S = kv.second;
+        for (void *p : S.opened) (void) hipIpcCloseMemHandle(p);
+        if (S.local) (void) hipFree(S.local);
+        for (int s = 0; s < 2; s++) {
+            if (S.ev_in[s]) (void) hipEventDestroy(S.ev_in[s]);
+            if (S.ev_out[s]) (void) hipEventDestroy(S.ev_out[s]);
+        }
+        if (S.st_in) (void) hipStreamDestroy(S.st_in);
+        if (S.st_c) (void) hipStreamDestroy(S.st_c);
+        if (S.st_out) (void) hipStreamDestroy(S.st_out);
+    }
+    g_stage.clear();
+    for (auto &kv : g_pectx) {
+        PeCtx *x = kv.second;
+        if (x->dscratch) (void) hipFree(x->dscratch);
+        if (x->hstage) (void) hipHostFree(x->hstage);
+        if (x->stream) (void) hipStreamDestroy(x->stream);
+        delete x;
+    }
+    g_pectx.clear();
+    (void) hipGetLastError();
+    return OSGPU_OK;
+}
+
+int osgpu_host_register(void *base, size_t bytes)
+{
+    hipError_t e = hipHostRegister(base, bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        set_err("hipHostRegister: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
+int osgpu_host_unregister(void *base)
+{
+    hipError_t e = hipHostUnregister(base);
+    if (e != hipSuccess) {
+        set_err("hipHostUnregister: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
 }
 
 int osgpu_set_path(int path)

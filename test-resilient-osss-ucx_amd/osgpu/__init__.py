@@ -104,6 +104,8 @@ def load() -> ctypes.CDLL:
     L.osgpu_shard_range.argtypes = [ctypes.c_longlong, i, i, i,
                                     ctypes.POINTER(ctypes.c_longlong),
                                     ctypes.POINTER(ctypes.c_longlong)]
+    L.osgpu_host_register.argtypes = [vp, sz]
+    L.osgpu_host_unregister.argtypes = [vp]
     L.osgpu_last_error.restype = ctypes.c_char_p
     L.osgpu_version.restype = ctypes.c_char_p
     _LIB = L

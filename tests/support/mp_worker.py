@@ -74,16 +74,20 @@ def main():
             src = np.ascontiguousarray(O.gen_input(t, n, O.pe_seed(0xDEF, rank), dist_))
             raw = src.view(np.uint8).reshape(-1)
             toff = (n * s + 4095) // 4096 * 4096
-            for inplace in (False, True):
+            # symmetric pSync at the top of the shared heap (the staged path
+            # exchanges its staging-buffer handles through spare pSync words)
+            psync = base + (1 << 24) - 4096
+            for hp, inplace in (("staged", False), ("staged", True), ("getmem", False)):
+                os.environ["OSGPU_HOST_PATH"] = hp
                 ctypes.memmove(base, raw.ctypes.data, raw.size)
                 tgt = base + (0 if inplace else toff)
-                psync = (ctypes.c_long * 128)()
                 wrk = (ctypes.c_byte * 4096)()
                 getattr(L, f"shmem_{t}_{op}_to_all")(tgt, base, n, 0, 0, world, wrk, psync)
                 got = np.frombuffer(ctypes.string_at(tgt, n * s), dtype=np.uint8)
                 if t == "longdouble":
                     got = got.reshape(-1, 16)[:, :10].reshape(-1)
-                out[f"{t}/{op}/host/{int(inplace)}"] = got.tobytes().hex()
+                out[f"{t}/{op}/{hp}/{int(inplace)}"] = got.tobytes().hex()
+                assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
                 dist.barrier()
         res["out"] = out
     if mode == "host":

@@ -123,7 +123,7 @@ typedef void (*to_all_fn)(void *, void *, int, int, int, int, void *, long *);
 typedef struct {
     to_all_fn fn;
     int npes, n, reps, me;
-    void **tgt, **src;
+    void **tgt, **src, **psync;
     pthread_barrier_t *bar;
     double *times;
 } timing_arg;
@@ -139,7 +139,8 @@ static double now_s(void)
 static void *timing_body(void *p)
 {
     timing_arg *a = (timing_arg *) p;
-    long psync[128] = {0};
+    long local_psync[128] = {0};
+    long *psync = a->psync ? (long *) a->psync[a->me] : local_psync;
     char wrk[4096];
     t_me = a->me;
     for (int r = 0; r <= a->reps; r++) {
@@ -158,7 +159,8 @@ static int cmpd(const void *x, const void *y)
     return a < b ? -1 : a > b;
 }
 
-double pet_time_to_all(void *fn, int npes, void **tgt, void **src, int n, int reps)
+double pet_time_to_all(void *fn, int npes, void **tgt, void **src, void **psync, int n,
+                       int reps)
 {
     if (npes < 1 || npes > MAXPE || reps < 1) return -1.0;
     pthread_barrier_t bar;
@@ -167,7 +169,7 @@ double pet_time_to_all(void *fn, int npes, void **tgt, void **src, int n, int re
     pthread_t th[MAXPE];
     timing_arg args[MAXPE];
     for (int i = 0; i < npes; i++) {
-        args[i] = (timing_arg){(to_all_fn) fn, npes, n, reps, i, tgt, src, &bar, times};
+        args[i] = (timing_arg){(to_all_fn) fn, npes, n, reps, i, tgt, src, psync, &bar, times};
         pthread_create(&th[i], NULL, timing_body, &args[i]);
     }
     for (int i = 0; i < npes; i++) pthread_join(th[i], NULL);

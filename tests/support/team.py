@@ -56,7 +56,9 @@ class Team:
         self.osgpu = osgpu
         self.pet = pet()
         self.npes = npes
-        self.H = _align(heap_bytes)
+        # the last 4 KiB of every PE's heap holds its symmetric pSync
+        self.H = _align(heap_bytes) + 4096
+        self.psync_off = self.H - 4096
         self.device = device
         assert self.pet.pet_init(npes) == 0
         assert self.lib.osgpu_set_pe_ops(self.pet.pet_ops()) == 0
@@ -120,12 +122,20 @@ class Team:
         pwrk = (ctypes.c_byte * 4096)()
         errs = []
 
+        def psync_ptr(pe):
+            # host heaps: symmetric pSync inside the heap (the staged host
+            # path reads peers' pSync words with getmem); device heaps: a host
+            # array (pSync is host memory in every OpenSHMEM program)
+            if self.device:
+                return ctypes.addressof(psync)
+            return self.ptr(pe, self.psync_off)
+
         def body(pe):
             try:
                 self.pet.pet_set_me(pe)
                 fn(self.ptr(pe, target_off), self.ptr(pe, source_off), nreduce,
                    PE_start, logPE_stride, PE_size, ctypes.addressof(pwrk),
-                   ctypes.addressof(psync))
+                   psync_ptr(pe))
             except Exception as e:  # pragma: no cover
                 errs.append(e)
 
@@ -137,6 +147,10 @@ class Team:
         if errs:
             raise errs[0]
         assert all(v == 0 for v in psync), "pSync must be left at SHMEM_SYNC_VALUE"
+        if not self.device:
+            for pe in members:
+                ps = self.hbuf[self.hoff + pe * self.H + self.psync_off:][:1024]
+                assert not ps.any(), "pSync must be left at SHMEM_SYNC_VALUE"
 
 
 X87_PATH = os.path.join(HERE, "libx87check.so")

@@ -129,8 +129,16 @@ def test_in_place_target_equals_source(torch_cuda, t, op):
 @pytest.mark.parametrize("t,op", [("int", "sum"), ("double", "sum"), ("long", "and"),
                                   ("float", "min"), ("complexd", "prod"),
                                   ("short", "prod"), ("longdouble", "prod")])
-def test_host_staged_matches_golden(torch_cuda, t, op, monkeypatch):
+@pytest.mark.parametrize("host_path", ["staged", "getmem"])
+def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
+    """Host symmetric heaps.  staged: H2D own source -> team exchange on the
+    GPU through the staging buffers -> D2H, 4 KiB chunks so the two-slot
+    pipeline turns over many times; getmem: every peer's source pulled
+    through the runtime's shmem_getmem (the reference's transport)."""
     monkeypatch.setenv("OSGPU_HOST_CHUNK_BYTES", "4096")  # many chunks
+    monkeypatch.setenv("OSGPU_STAGE_BYTES", "4096")
+    monkeypatch.setenv("OSGPU_HOST_PATH", host_path)
+    osgpu.load().osgpu_finalize()  # staging is sized at set-up
     tm = team(device=False)
     n = 0
     for c in CASES:
@@ -142,6 +150,7 @@ def test_host_staged_matches_golden(torch_cuda, t, op, monkeypatch):
     c = next(c for c in CASES if c["type"] == t and c["op"] == op and c["npes"] == 3
              and c["nreduce"] == 4097 and c["tag"] == "grid")
     check(c, run_case(tm, c, in_place=True))
+    osgpu.load().osgpu_finalize()
 
 
 def _stream(torch):

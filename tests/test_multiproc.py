@@ -93,12 +93,15 @@ def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-def test_host_staged_processes(tmp_path, world):
-    """Host symmetric heaps (shared memory), getmem between processes, the
-    combine on the GPU: the reference's own data placement."""
+def test_host_staged_processes(tmp_path, world, monkeypatch):
+    """Host symmetric heaps (shared memory), one process per PE -- the
+    reference's own data placement.  STAGED: H2D -> exchange through the
+    IPC-mapped staging buffers -> D2H (64 KiB chunks: many pipeline turns);
+    GETMEM: peers' sources pulled through the runtime's getmem."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("OSGPU_STAGE_BYTES", "65536")
     res = launch("hoststaged", world, tmp_path)
     specs = (("double", "sum", 300_007, "wide"), ("float", "max", 4097, "edge"),
              ("long", "or", 65, "or"), ("complexf", "prod", 1000, "edge"),
