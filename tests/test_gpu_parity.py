@@ -153,8 +153,17 @@ def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
     osgpu.load().osgpu_finalize()
 
 
+_S = []
+
+
 def _stream(torch):
-    return torch.cuda.current_stream().cuda_stream
+    """A non-default torch stream, after draining the device: torch's default
+    stream has handle 0, and a NULL stream means "the calling thread's
+    stream" to osgpu_combine, which would not be ordered after torch's work."""
+    torch.cuda.synchronize()
+    if not _S:
+        _S.append(torch.cuda.Stream())
+    return _S[0].cuda_stream
 
 
 def _dev(torch, arr):
