@@ -52,6 +52,10 @@ def parse():
                          "rccl is measured after it unless --no-rccl")
     ap.add_argument("--no-rccl", action="store_true")
     ap.add_argument("--rccl-timeout", type=float, default=240.0)
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N>1: skip the config-4 (1 Gi) and config-5 (host, float) runs")
+    ap.add_argument("--c4-nreduce", type=int, default=1 << 30)
+    ap.add_argument("--c5-nreduce", type=int, default=128 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=64 << 20,
@@ -252,7 +256,7 @@ def bench_single(args):
     print(json.dumps(res), flush=True)
 
 
-def _sample_parity(L, rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15):
+def _sample_parity(L, rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15, t="double"):
     """Bit-exact check of this PE's target on a sample of elements: every
     rank contributes its source at the sampled indices (gloo), the oracle
     folds them in this PE's order (src/reductions.c:79-111)."""
@@ -265,9 +269,10 @@ def _sample_parity(L, rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15):
     allv = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(allv, mine)
     srcs = [a.numpy() for a in allv]
-    want = O.fold_with(O.op_elementwise, "double", fn_op, srcs, rank, 0, 0, world)
+    want = O.fold_with(O.op_elementwise, t, fn_op, srcs, rank, 0, 0, world)
     got = tgt[idx.to(tgt.device)].cpu().numpy()
-    bad = int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))
+    ui = np.uint64 if t == "double" else np.uint32
+    bad = int(np.count_nonzero(got.view(ui) != want.view(ui)))
     rel = float(np.max(np.abs(got - want) / np.abs(want))) if nsamp else 0.0
     return {"checked": nsamp, "bit_mismatches": bad, "max_rel_err": rel}
 
@@ -310,35 +315,41 @@ def bench_multi(args):
     n = args.nreduce
     dev = torch.device("cuda", dev_id)
 
-    off_t = (n * 8 + 4095) // 4096 * 4096
-    H = off_t + n * 8
-    heap = torch.empty(H, dtype=torch.uint8, device=dev)
-    src = heap[: n * 8].view(torch.float64)
-    tgt = heap[off_t: off_t + n * 8].view(torch.float64)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    src.uniform_(1.0, 2.0, generator=g)
-    torch.cuda.synchronize()
     psync = (ctypes.c_long * 128)()
     wrk = (ctypes.c_double * 64)()
     fn = L.shmem_double_sum_to_all
 
+    def device_heap(nn, seed):
+        """Symmetric device heap [source | target] of nn doubles, exported
+        over IPC and every peer's registered (osgpu_heap_register)."""
+        off_t = (nn * 8 + 4095) // 4096 * 4096
+        H = off_t + nn * 8
+        heap = torch.empty(H, dtype=torch.uint8, device=dev)
+        s_ = heap[: nn * 8].view(torch.float64)
+        t_ = heap[off_t: off_t + nn * 8].view(torch.float64)
+        s_.uniform_(1.0, 2.0, generator=torch.Generator(device=dev).manual_seed(seed + rank))
+        torch.cuda.synchronize()
+        h = (ctypes.c_char * 64)()
+        assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
+        hs = [None] * world
+        dist.all_gather_object(hs, bytes(h))
+        maps = []
+        for pe in range(world):
+            if pe == rank:
+                base = heap.data_ptr()
+            else:
+                base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(hs[pe]))
+                assert base, L.osgpu_last_error().decode()
+                maps.append(base)
+            assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), H) == 0
+        return heap, s_, t_, maps
+
+    # ---- primary: exact team kernel over IPC-mapped heaps
+    heap, src, tgt, mapped = device_heap(n, 1000)
+
     def step():
         fn(tgt.data_ptr(), src.data_ptr(), n, 0, 0, world, wrk, psync)
 
-    # ---- primary: exact team kernel over IPC-mapped heaps
-    h = (ctypes.c_char * 64)()
-    assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
-    hs = [None] * world
-    dist.all_gather_object(hs, bytes(h))
-    mapped = []
-    for pe in range(world):
-        if pe == rank:
-            base = heap.data_ptr()
-        else:
-            base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(hs[pe]))
-            assert base, L.osgpu_last_error().decode()
-            mapped.append(base)
-        assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), H) == 0
     L.osgpu_set_path(osgpu.PATH_P2P)
     t = _timed(step, args.steps, args.warmup, dist, torch)
     parity = _sample_parity(L, rank, world, src, tgt, n, "sum", dist)
@@ -370,6 +381,59 @@ def bench_multi(args):
     }
     out = {"res": res}
     printed = threading.Event()
+
+    # ---- BASELINE config 4: nreduce = 1 Gi doubles per PE (8 GiB), team path
+    if not args.no_extra:
+        try:
+            n4 = args.c4_nreduce
+            heap4, s4, t4, maps4 = device_heap(n4, 4000)
+
+            def step4():
+                fn(t4.data_ptr(), s4.data_ptr(), n4, 0, 0, world, wrk, psync)
+
+            tt = _timed(step4, 3, 1, dist, torch)
+            p4 = _sample_parity(L, rank, world, s4, t4, n4, "sum", dist)
+            pl = [None] * world
+            dist.all_gather_object(pl, p4)
+            res["config4"] = {"nreduce": n4, "ms_per_call": tt / 3 * 1e3,
+                              "value_GiBs": 3 * (world + 1) * n4 * 8 / tt / GIB,
+                              "algbw_GiBs": 3 * n4 * 8 / tt / GIB,
+                              "bit_mismatches": sum(p["bit_mismatches"] for p in pl)}
+            dist.barrier()
+            for p in maps4:
+                L.osgpu_ipc_close(ctypes.c_void_p(p))
+            del heap4, s4, t4
+            torch.cuda.empty_cache()
+        except Exception as e:
+            res["config4"] = {"error": repr(e)[:300]}
+
+    # ---- BASELINE config 5: float min/max/prod, nreduce = 128 Mi per PE,
+    # sources/targets in pinned HOST memory: H2D + on-GPU exchange + D2H
+    if not args.no_extra:
+        try:
+            n5 = args.c5_nreduce
+            hsrc = torch.empty(n5, dtype=torch.float32).pin_memory()
+            htgt = torch.empty(n5, dtype=torch.float32).pin_memory()
+            ps = PES.pes_heap(rank) + (1 << 20) - 4096   # symmetric pSync
+            g5 = torch.Generator().manual_seed(77 + rank)
+            c5 = {"nreduce": n5, "placement": "pinned host memory, STAGED path"}
+            for op, lo, hi in (("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1)):
+                hsrc.uniform_(lo, hi, generator=g5)
+                f5 = getattr(L, f"shmem_float_{op}_to_all")
+
+                def step5():
+                    f5(htgt.data_ptr(), hsrc.data_ptr(), n5, 0, 0, world, wrk, ps)
+
+                tt = _timed(step5, 3, 1, dist, torch)
+                p5 = _sample_parity(L, rank, world, hsrc, htgt, n5, op, dist, t="float")
+                pl = [None] * world
+                dist.all_gather_object(pl, p5)
+                c5[op] = {"ms_per_call": tt / 3 * 1e3,
+                          "GiBs_per_PE_incl_H2D_D2H": 3 * n5 * 4 / tt / GIB,
+                          "bit_mismatches": sum(p["bit_mismatches"] for p in pl)}
+            res["config5"] = c5
+        except Exception as e:
+            res["config5"] = {"error": repr(e)[:300]}
 
     def emit():
         if rank == 0 and not printed.is_set():
