@@ -277,6 +277,10 @@ def _sample_parity(L, rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15, t="d
     return {"checked": nsamp, "bit_mismatches": bad, "max_rel_err": rel}
 
 
+def _log(rank, msg):
+    print(f"[bench rank {rank}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def _timed(step, steps, warmup, dist, torch):
     for _ in range(warmup):
         step()
@@ -329,10 +333,12 @@ def bench_multi(args):
         t_ = heap[off_t: off_t + nn * 8].view(torch.float64)
         s_.uniform_(1.0, 2.0, generator=torch.Generator(device=dev).manual_seed(seed + rank))
         torch.cuda.synchronize()
+        _log(rank, f"heap of {H} B allocated")
         h = (ctypes.c_char * 64)()
         assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
         hs = [None] * world
         dist.all_gather_object(hs, bytes(h))
+        _log(rank, "ipc handles exchanged")
         maps = []
         for pe in range(world):
             if pe == rank:
@@ -351,8 +357,11 @@ def bench_multi(args):
         fn(tgt.data_ptr(), src.data_ptr(), n, 0, 0, world, wrk, psync)
 
     L.osgpu_set_path(osgpu.PATH_P2P)
+    _log(rank, "primary heap ready")
     t = _timed(step, args.steps, args.warmup, dist, torch)
+    _log(rank, "primary timed")
     parity = _sample_parity(L, rank, world, src, tgt, n, "sum", dist)
+    _log(rank, "primary parity checked")
     pars = [None] * world
     dist.all_gather_object(pars, parity)
     B = (world + 1) * n * 8          # sum over GPUs of shard-fold bytes
@@ -391,6 +400,7 @@ def bench_multi(args):
             def step4():
                 fn(t4.data_ptr(), s4.data_ptr(), n4, 0, 0, world, wrk, psync)
 
+            _log(rank, "config4 heap ready")
             tt = _timed(step4, 3, 1, dist, torch)
             p4 = _sample_parity(L, rank, world, s4, t4, n4, "sum", dist)
             pl = [None] * world
@@ -407,6 +417,7 @@ def bench_multi(args):
         except Exception as e:
             res["config4"] = {"error": repr(e)[:300]}
 
+    _log(rank, "config4 done")
     # ---- BASELINE config 5: float min/max/prod, nreduce = 128 Mi per PE,
     # sources/targets in pinned HOST memory: H2D + on-GPU exchange + D2H
     if not args.no_extra:
@@ -424,6 +435,7 @@ def bench_multi(args):
                 def step5():
                     f5(htgt.data_ptr(), hsrc.data_ptr(), n5, 0, 0, world, wrk, ps)
 
+                _log(rank, f"config5 {op} start")
                 tt = _timed(step5, 3, 1, dist, torch)
                 p5 = _sample_parity(L, rank, world, hsrc, htgt, n5, op, dist, t="float")
                 pl = [None] * world
@@ -440,6 +452,7 @@ def bench_multi(args):
             printed.set()
             print(json.dumps(out["res"]), flush=True)
 
+    _log(rank, "config5 done")
     # ---- secondary: RCCL allreduce (guarded)
     if args.path == "rccl" or not args.no_rccl:
         def watchdog():
@@ -468,6 +481,7 @@ def bench_multi(args):
         except Exception as e:  # reported, never hidden
             res["rccl"] = {"error": repr(e)[:300]}
         done.set()
+    _log(rank, "rccl phase done")
     emit()
     L.osgpu_set_path(osgpu.PATH_AUTO)
     dist.barrier()

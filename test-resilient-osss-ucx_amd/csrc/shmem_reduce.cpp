@@ -67,6 +67,28 @@ void set_err(const char *fmt, ...)
     abort();
 }
 
+// OSGPU_DEBUG=1: one stderr line per protocol step (call entry, path,
+// barriers, launches, syncs) -- for diagnosing multi-process runs
+int debug_level()
+{
+    static int lvl = -1;
+    if (lvl < 0) {
+        const char *e = getenv("OSGPU_DEBUG");
+        lvl = e ? atoi(e) : 0;
+    }
+    return lvl;
+}
+
+#define DBG(...)                                                               \
+    do {                                                                       \
+        if (debug_level() > 0) {                                               \
+            fprintf(stderr, "[osgpu pid %d] ", (int) getpid());                \
+            fprintf(stderr, __VA_ARGS__);                                      \
+            fputc('\n', stderr);                                               \
+            fflush(stderr);                                                    \
+        }                                                                      \
+    } while (0)
+
 #define HIPCHK(where, call)                                                    \
     do {                                                                       \
         hipError_t e_ = (call);                                                \
@@ -133,17 +155,49 @@ PeOps pe_ops()
 
 // -------------------------------------------------------- device sym. heap
 
+// A PE's device heap is one or more segments (separate allocations: HIP IPC
+// cannot export a single allocation of 2 GiB or more on this platform, see
+// DESIGN.md 6).  A symmetric object lives in the same segment at the same
+// offset on every PE.
 struct HeapEntry {
     char *base = nullptr;
     size_t bytes = 0;
 };
-std::vector<HeapEntry> g_heap;  // indexed by PE
+std::vector<std::vector<HeapEntry>> g_heap;  // [PE][segment]
 
-bool heap_lookup(int pe, HeapEntry *out)
+bool heap_segment(int pe, int seg, HeapEntry *out)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (pe < 0 || (size_t) pe >= g_heap.size() || !g_heap[pe].base) return false;
-    *out = g_heap[pe];
+    if (pe < 0 || (size_t) pe >= g_heap.size() || seg < 0 ||
+        (size_t) seg >= g_heap[pe].size() || !g_heap[pe][seg].base)
+        return false;
+    *out = g_heap[pe][seg];
+    return true;
+}
+
+// segment of PE `pe` holding [addr, addr + nbytes), and the offset in it
+bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (pe < 0 || (size_t) pe >= g_heap.size()) return false;
+    const char *p = (const char *) addr;
+    for (size_t s = 0; s < g_heap[pe].size(); s++) {
+        const HeapEntry &h = g_heap[pe][s];
+        if (h.base && p >= h.base && p + nbytes <= h.base + h.bytes) {
+            *seg = (int) s;
+            *off = (size_t) (p - h.base);
+            return true;
+        }
+    }
+    return false;
+}
+
+// address of the symmetric object at (seg, off) on PE pe, checked for nbytes
+bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out)
+{
+    HeapEntry h;
+    if (!heap_segment(pe, seg, &h) || off + nbytes > h.bytes) return false;
+    *out = h.base + off;
     return true;
 }
 
@@ -298,23 +352,23 @@ struct Call {
 
 void barrier(const Call &c)
 {
+    DBG("%s PE %d: barrier enter", c.name, c.me);
     c.ops.barrier(c.PE_start, c.logPE_stride, c.PE_size, c.pSync);
+    DBG("%s PE %d: barrier exit", c.name, c.me);
 }
 
 bool p2p_sources(const Call &c, std::vector<const void *> &srcs)
 {
-    HeapEntry mine;
-    if (!heap_lookup(c.me, &mine)) return false;
-    const char *s = (const char *) c.source;
-    if (s < mine.base || s + c.nbytes > mine.base + mine.bytes) return false;
-    const size_t off = (size_t) (s - mine.base);
+    int seg = -1;
+    size_t off = 0;
+    if (!heap_locate(c.me, c.source, c.nbytes, &seg, &off)) return false;
     std::vector<int> order(c.PE_size);
     fold_order(c.me, c.PE_start, c.step, c.PE_size, order.data());
     srcs.resize(c.PE_size);
     for (int k = 0; k < c.PE_size; k++) {
-        HeapEntry h;
-        if (!heap_lookup(order[k], &h) || off + c.nbytes > h.bytes) return false;
-        srcs[k] = h.base + off;
+        char *p = nullptr;
+        if (!heap_peer(order[k], seg, off, c.nbytes, &p)) return false;
+        srcs[k] = p;
     }
     return true;
 }
@@ -327,21 +381,19 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
 {
     if (c.PE_size < 2 || c.PE_size > osgpu::kMaxTeam) return -1;
     if (ranges_overlap(c.target, c.source, c.nbytes)) return -1;
-    HeapEntry mine;
-    if (!heap_lookup(c.me, &mine)) return -1;
-    const char *s = (const char *) c.source, *t = (const char *) c.target;
-    if (s < mine.base || s + c.nbytes > mine.base + mine.bytes) return -1;
-    if (t < mine.base || t + c.nbytes > mine.base + mine.bytes) return -1;
-    const size_t os = (size_t) (s - mine.base), ot = (size_t) (t - mine.base);
+    int ss = -1, st = -1;
+    size_t os = 0, ot = 0;
+    if (!heap_locate(c.me, c.source, c.nbytes, &ss, &os)) return -1;
+    if (!heap_locate(c.me, c.target, c.nbytes, &st, &ot)) return -1;
     srcs.resize(c.PE_size);
     dsts.resize(c.PE_size);
     int idx = -1;
     for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
-        HeapEntry h;
-        if (!heap_lookup(pe, &h) || os + c.nbytes > h.bytes || ot + c.nbytes > h.bytes)
+        char *sp = nullptr, *tp = nullptr;
+        if (!heap_peer(pe, ss, os, c.nbytes, &sp) || !heap_peer(pe, st, ot, c.nbytes, &tp))
             return -1;
-        srcs[i] = h.base + os;
-        dsts[i] = h.base + ot;
+        srcs[i] = sp;
+        dsts[i] = tp;
         if (pe == c.me) idx = i;
     }
     return idx;
@@ -360,6 +412,8 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
         sp[i] = (const char *) srcs[i] + (size_t) lo * s;
         dp[i] = (char *) dsts[i] + (size_t) lo * s;
     }
+    DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
+        c.nreduce, c.PE_size);
     HIPCHK(c.name, hipDeviceSynchronize());
     barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
     if (hi > lo) {
@@ -367,7 +421,9 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
                                           (size_t) (hi - lo), st);
         if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
     }
+    DBG("%s PE %d: team kernel launched", c.name, c.me);
     HIPCHK(c.name, hipStreamSynchronize(st));
+    DBG("%s PE %d: team kernel done", c.name, c.me);
     barrier(c);  // src/reductions.c:113 -- every shard of my target is written
 }
 
@@ -842,35 +898,41 @@ int osgpu_set_pe_ops(const osgpu_pe_ops *ops)
     return OSGPU_OK;
 }
 
-int osgpu_heap_register(int pe, void *base, size_t bytes)
+int osgpu_heap_register_segment(int pe, int seg, void *base, size_t bytes)
 {
-    if (pe < 0 || !base || !bytes) {
-        set_err("osgpu_heap_register: bad arguments");
+    if (pe < 0 || seg < 0 || seg > 255 || !base || !bytes) {
+        set_err("osgpu_heap_register_segment: bad arguments");
         return OSGPU_EINVAL;
     }
     std::lock_guard<std::mutex> lk(g_mu);
     if ((size_t) pe >= g_heap.size()) g_heap.resize(pe + 1);
-    g_heap[pe].base = (char *) base;
-    g_heap[pe].bytes = bytes;
+    if ((size_t) seg >= g_heap[pe].size()) g_heap[pe].resize(seg + 1);
+    g_heap[pe][seg].base = (char *) base;
+    g_heap[pe][seg].bytes = bytes;
     return OSGPU_OK;
+}
+
+int osgpu_heap_register(int pe, void *base, size_t bytes)
+{
+    return osgpu_heap_register_segment(pe, 0, base, bytes);
 }
 
 int osgpu_heap_unregister(int pe)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (pe < 0 || (size_t) pe >= g_heap.size()) return OSGPU_EINVAL;
-    g_heap[pe] = HeapEntry();
+    g_heap[pe].clear();
     return OSGPU_OK;
 }
 
 void *osgpu_heap_translate(const void *addr, int from_pe, int to_pe)
 {
-    HeapEntry a, b;
-    if (!heap_lookup(from_pe, &a) || !heap_lookup(to_pe, &b)) return nullptr;
-    const char *p = (const char *) addr;
-    if (p < a.base || p >= a.base + a.bytes) return nullptr;
-    size_t off = (size_t) (p - a.base);
-    return off < b.bytes ? b.base + off : nullptr;
+    int seg = -1;
+    size_t off = 0;
+    char *p = nullptr;
+    if (!heap_locate(from_pe, addr, 1, &seg, &off) || !heap_peer(to_pe, seg, off, 1, &p))
+        return nullptr;
+    return p;
 }
 
 int osgpu_ipc_get_handle(void *dev_base, void *handle_out)

@@ -84,6 +84,7 @@ def load() -> ctypes.CDLL:
             f.restype = None
     L.osgpu_set_pe_ops.argtypes = [vp]
     L.osgpu_heap_register.argtypes = [i, vp, sz]
+    L.osgpu_heap_register_segment.argtypes = [i, i, vp, sz]
     L.osgpu_heap_unregister.argtypes = [i]
     L.osgpu_heap_translate.argtypes = [vp, i, i]
     L.osgpu_heap_translate.restype = vp
