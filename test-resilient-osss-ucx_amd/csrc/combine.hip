@@ -48,7 +48,7 @@ constexpr int kBlock = 256;
 // lanes per vector-tile unroll: keep K*U*4 VGPRs of payload modest
 template <int K>
 struct Unroll {
-    static constexpr int value = K <= 2 ? 4 : (K <= 4 ? 2 : 1);
+    static constexpr int value = K <= 2 ? OSGPU_U_K2 : (K <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
 };
 
 template <typename T, int OP, int K>

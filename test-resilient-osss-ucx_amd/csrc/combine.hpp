@@ -3,6 +3,18 @@
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
 
+// 16-byte vectors in flight per lane per input: for <= 2, <= 4 and <= 8
+// inputs (register budget vs bytes in flight; see tools/tune_combine.hip)
+#ifndef OSGPU_U_K2
+#define OSGPU_U_K2 4
+#endif
+#ifndef OSGPU_U_K4
+#define OSGPU_U_K4 4
+#endif
+#ifndef OSGPU_U_K8
+#define OSGPU_U_K8 2
+#endif
+
 namespace osgpu {
 
 // type codes (same numbering as include/osgpu_reduce.h OSGPU_T_*)

@@ -55,6 +55,71 @@ __device__ __forceinline__ X80 apply(X80 a, X80 b)
 
 constexpr int kMaxIn = 8;
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ X80 unpack(u64x2 v) { return X80{v.x, (uint32_t) (v.y & 0xffffu)}; }
+__device__ __forceinline__ u64x2 pack(X80 x)
+{
+    u64x2 v;
+    v.x = x.m;
+    v.y = (unsigned long long) (x.se & 0xffffu);  // padding bytes written as zero
+    return v;
+}
+
+template <int K>
+struct LdVecInputs {
+    const u64x2 *p[K];
+};
+
+// 16-byte aligned arrays: one dwordx4 per element per input, U elements per
+// lane with every load issued before the soft-float fold
+template <int OP, int K>
+__global__ __launch_bounds__(256) void ld_vec_kernel(u64x2 *out, LdVecInputs<K> in, size_t n)
+{
+    constexpr int U = K <= 2 ? 4 : 2;
+    const size_t base = (size_t) blockIdx.x * (256 * U) + threadIdx.x;
+    u64x2 raw[U][K];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t) u * 256;
+        if (i < n) {
+#pragma unroll
+            for (int k = 0; k < K; k++) raw[u][k] = __builtin_nontemporal_load(in.p[k] + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t) u * 256;
+        if (i < n) {
+            X80 acc = unpack(raw[u][0]);
+#pragma unroll
+            for (int k = 1; k < K; k++) acc = apply<OP>(acc, unpack(raw[u][k]));
+            __builtin_nontemporal_store(pack(acc), out + i);
+        }
+    }
+}
+
+template <int OP>
+static hipError_t ld_vec_launch(int K, void *out, const void *const *srcs, size_t n,
+                                hipStream_t s)
+{
+#define LDV(KK)                                                                \
+    case KK: {                                                                 \
+        LdVecInputs<KK> in;                                                    \
+        for (int k = 0; k < KK; k++) in.p[k] = (const u64x2 *) srcs[k];        \
+        constexpr int U = KK <= 2 ? 4 : 2;                                     \
+        size_t blocks = (n + 256 * U - 1) / (256 * U);                         \
+        hipLaunchKernelGGL((ld_vec_kernel<OP, KK>), dim3((unsigned) (blocks ? blocks : 1)), \
+                           dim3(256), 0, s, (u64x2 *) out, in, n);             \
+        return hipGetLastError();                                              \
+    }
+    switch (K) {
+        LDV(1) LDV(2) LDV(3) LDV(4) LDV(5) LDV(6) LDV(7) LDV(8)
+    }
+#undef LDV
+    return hipErrorInvalidValue;
+}
+
 struct LdInputs {
     const unsigned char *p[kMaxIn];
 };
@@ -92,6 +157,21 @@ hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, 
         if (!first) in.p[m++] = (const unsigned char *) out;
         while (m < x87::kMaxIn && done < k) in.p[m++] = (const unsigned char *) srcs[done++];
         first = false;
+        bool aligned16 = ((uintptr_t) out & 15) == 0;
+        for (int j = 0; j < m; j++) aligned16 = aligned16 && ((uintptr_t) in.p[j] & 15) == 0;
+        if (aligned16) {  // the usual case: x86-64 long double arrays are 16-B aligned
+            const void *vp[x87::kMaxIn];
+            for (int j = 0; j < m; j++) vp[j] = in.p[j];
+            hipError_t e;
+            switch (op) {
+            case 0: e = x87::ld_vec_launch<0>(m, out, vp, n, s); break;
+            case 1: e = x87::ld_vec_launch<1>(m, out, vp, n, s); break;
+            case 5: e = x87::ld_vec_launch<5>(m, out, vp, n, s); break;
+            default: e = x87::ld_vec_launch<6>(m, out, vp, n, s); break;
+            }
+            if (e != hipSuccess) return e;
+            continue;
+        }
         switch (op) {
         case 0: hipLaunchKernelGGL(x87::ld_combine_kernel<0>, dim3((unsigned) blocks), dim3(256), 0, s,
                                    (unsigned char *) out, in, m, n); break;

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                                                               int nedge)
 {
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
+    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -141,7 +141,7 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
+    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
     size_t head = phase ? (16 - phase) / sizeof(T) : 0;
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;

@@ -14,7 +14,8 @@ import os
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libosgpu_reduce.so")
+# OSGPU_LIB_PATH: load another build of the same library (tuning tools only)
+LIB_PATH = os.environ.get("OSGPU_LIB_PATH") or os.path.join(PKG_DIR, "libosgpu_reduce.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 REPO = os.path.dirname(PKG_DIR)
 HEADER = os.path.join(REPO, "include", "osgpu_reduce.h")

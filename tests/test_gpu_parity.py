@@ -204,6 +204,26 @@ def test_combine_ragged_and_misaligned(torch_cuda, t, k):
             assert bad.size == 0, (t, k, n, shift_in, shift_out, bad[:8] // s)
 
 
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min"])
+def test_longdouble_8byte_aligned_arrays(torch_cuda, op):
+    """long double arrays that are only 8-byte aligned take the scalar
+    soft-float kernel (the usual 16-byte-aligned ones the vector kernel)."""
+    torch = torch_cuda
+    n, k = 1001, 3
+    ins = [O.gen_input("longdouble", n, 77 + j, "edge") for j in range(k)]
+    want = ins[0]
+    for x in ins[1:]:
+        want = O.op_elementwise("longdouble", op, want, x)
+    bufs = [_dev(torch, np.concatenate([np.zeros(8, np.uint8), x.view(np.uint8)]))
+            for x in ins]
+    out = torch.zeros(n * 16 + 8, dtype=torch.uint8, device="cuda:0")
+    osgpu.combine("longdouble", op, out.data_ptr() + 8, [b.data_ptr() + 8 for b in bufs], n,
+                  _stream(torch))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()[8:].reshape(-1, 16)[:, :10].reshape(-1)
+    assert np.array_equal(got, O.value_bytes(want).reshape(-1))
+
+
 def test_large_config2_shape_properties(torch_cuda):
     """BASELINE config 2 at full size (nreduce = 64 Mi doubles, 2 inputs):
     checked against the oracle on a strided sample and through the exact
