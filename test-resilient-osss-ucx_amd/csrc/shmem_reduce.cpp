@@ -5,20 +5,24 @@
 // with the same 44 signatures.  Where the reference walks its peers with a
 // blocking 64-element shmem_getmem per chunk and folds through a function
 // pointer per element (udr_<T>_to_all, src/reductions.c:32-120), this layer
-// picks one of three MI355X paths:
+// picks one of these MI355X paths:
 //
-//   P2P   (device-resident, every active PE's device heap addressable here):
-//         the reference's pull schedule as ONE combine kernel that streams
-//         all PE_size sources -- local HBM or peer HBM over xGMI -- in the
-//         reference's fold order (bit-exact, including floating point);
-//   RCCL  (device-resident, one process per GPU with an RCCL communicator):
-//         ncclAllReduce over xGMI stands in for the barrier + pull schedule;
-//   HOST  (host symmetric-heap arguments): peers' sources staged through the
-//         runtime's shmem_getmem (UCX) into pinned buffers, H2D, the same
-//         combine kernel, D2H.
+//   TEAM    device-resident, source and target symmetric in registered
+//           heaps, 2..8 PEs: owner-computes kernel (team.hip) -- PE g folds
+//           shard g of every PE's target, each in that PE's own fold order,
+//           reading every source once over HBM/xGMI (bit-exact);
+//   PULL    device-resident, source symmetric: the reference's pull
+//           schedule as ONE combine kernel streaming all PE_size sources in
+//           the PE's fold order (bit-exact);
+//   RCCL    device-resident, one process per GPU with an RCCL communicator:
+//           ncclAllReduce over xGMI (FP within tolerance);
+//   STAGED  host symmetric-heap arguments: H2D own source -> TEAM over
+//           IPC-mapped device staging -> D2H, pipelined (bit-exact);
+//   GETMEM  host arguments when staging cannot be mapped by every PE: peers'
+//           sources pulled with the runtime's shmem_getmem, H2D, combine, D2H.
 //
 // The two shmem_barrier calls of the reference (:82, :113) keep their roles
-// on the P2P and HOST paths (sources ready / peers done reading).
+// (every source ready / every reader or writer done) on every non-RCCL path.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 

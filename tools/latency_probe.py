@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-call latency of shmem_int_sum_to_all at small nreduce (BASELINE
+config 1 shape: 2 PEs), device-resident (team / pull paths) and
+host-resident (staged path), timed in C (pet_time_to_all), next to the CPU
+reference loop shape.  Not part of the product."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
+    sys.path.insert(0, os.path.join(ROOT, sub))
+
+import numpy as np  # noqa: E402
+import osgpu  # noqa: E402
+import oracle as O  # noqa: E402
+from support import team as T  # noqa: E402
+
+sig = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+       ctypes.c_int, ctypes.c_int]
+out = {}
+for n in (1024, 65536, 1 << 20):
+    row = {}
+    for device in (True, False):
+        tm = T.Team(2, 2 * n * 4 + 8192, device=device)
+        tm.pet.pet_time_to_all.restype = ctypes.c_double
+        tm.pet.pet_time_to_all.argtypes = sig
+        toff = (n * 4 + 4095) // 4096 * 4096
+        fn = ctypes.cast(tm.lib.shmem_int_sum_to_all, ctypes.c_void_p)
+        tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
+        src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
+        if device:
+            for name, path in (("team", osgpu.PATH_AUTO), ("pull", osgpu.PATH_PULL)):
+                tm.lib.osgpu_set_path(path)
+                row[name + "_us"] = tm.pet.pet_time_to_all(fn, 2, tgt, src, None, n, 200) * 1e6
+            tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
+        else:
+            ps = (ctypes.c_void_p * 2)(tm.ptr(0, tm.psync_off), tm.ptr(1, tm.psync_off))
+            row["host_staged_us"] = tm.pet.pet_time_to_all(fn, 2, tgt, src, ps, n, 200) * 1e6
+        tm.lib.osgpu_finalize()
+        del tm
+    srcs = O.team_inputs("int", 2, n, 5, "bits")
+    row["cpu_reference_loop_us"] = O.cpu_baseline("int", "sum", srcs, reps=200, pin=True) * 1e6
+    out[n] = row
+    print(json.dumps({"nreduce": n, **row}), flush=True)
