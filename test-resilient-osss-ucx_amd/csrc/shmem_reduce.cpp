@@ -99,6 +99,39 @@ int debug_level()
         if (e_ != hipSuccess) fatal(where, "%s: %s", #call, hipGetErrorString(e_)); \
     } while (0)
 
+// ----------------------------------------------------------- synchronisation
+
+int env_choice(const char *var, const char *alt, int def_is_alt)
+{
+    const char *e = getenv(var);
+    if (!e) return def_is_alt;
+    return strcmp(e, alt) == 0;
+}
+
+// Entry: device work this process enqueued earlier (on any stream) may still
+// be producing `source`; the collective reads it only after it is done.
+// OSGPU_ENTRY_SYNC=none skips this for callers that synchronise themselves.
+void entry_sync(const char *where)
+{
+    static const int skip = env_choice("OSGPU_ENTRY_SYNC", "none", 0);
+    if (!skip) HIPCHK(where, hipDeviceSynchronize());
+}
+
+// Completion of our own stream: poll (default; the combine is short and the
+// wake-up latency of a blocking wait is a large share of a small call) or
+// block (OSGPU_SYNC=block).
+void stream_wait(const char *where, hipStream_t st)
+{
+    static const int block = env_choice("OSGPU_SYNC", "block", 0);
+    if (block) {
+        HIPCHK(where, hipStreamSynchronize(st));
+        return;
+    }
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+    if (e != hipSuccess) fatal(where, "stream: %s", hipGetErrorString(e));
+}
+
 // --------------------------------------------------------------- type info
 
 size_t type_size(int t)
@@ -418,7 +451,7 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     }
     DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
         c.nreduce, c.PE_size);
-    HIPCHK(c.name, hipDeviceSynchronize());
+    entry_sync(c.name);
     barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
     if (hi > lo) {
         hipError_t e = osgpu::launch_team(c.type, c.op, c.PE_size, dp.data(), sp.data(),
@@ -426,7 +459,7 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
         if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
     }
     DBG("%s PE %d: team kernel launched", c.name, c.me);
-    HIPCHK(c.name, hipStreamSynchronize(st));
+    stream_wait(c.name, st);
     DBG("%s PE %d: team kernel done", c.name, c.me);
     barrier(c);  // src/reductions.c:113 -- every shard of my target is written
 }
@@ -435,18 +468,18 @@ void run_p2p(const Call &c, const std::vector<const void *> &srcs)
 {
     hipStream_t st = pe_stream(c.name, c.me);
     // prior device work of this process that produced `source` must be done
-    HIPCHK(c.name, hipDeviceSynchronize());
+    entry_sync(c.name);
     barrier(c);  // src/reductions.c:82 -- every source is ready
     const bool overlap = c.PE_size > 1 && ranges_overlap(c.target, c.source, c.nbytes);
     void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
     hipError_t e = osgpu::launch_combine(c.type, c.op, out, srcs.data(), c.PE_size,
                                          (size_t) c.nreduce, st);
     if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
-    HIPCHK(c.name, hipStreamSynchronize(st));
+    stream_wait(c.name, st);
     barrier(c);  // src/reductions.c:113 -- peers are done reading my source
     if (overlap) {
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
-        HIPCHK(c.name, hipStreamSynchronize(st));
+        stream_wait(c.name, st);
     }
 }
 
@@ -490,16 +523,16 @@ void run_rccl(const Call &c)
     size_t mult;
     rccl_types(c.type, c.op, &dt, &rop, &mult);
     hipStream_t st = pe_stream(c.name, c.me);
-    HIPCHK(c.name, hipDeviceSynchronize());
+    entry_sync(c.name);
     const bool overlap = ranges_overlap(c.target, c.source, c.nbytes) && c.target != c.source;
     void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
     ncclResult_t r = ncclAllReduce(c.source, out, (size_t) c.nreduce * mult, dt, rop,
                                    g_rccl.world, st);
     if (r != ncclSuccess) fatal(c.name, "ncclAllReduce: %s", ncclGetErrorString(r));
-    HIPCHK(c.name, hipStreamSynchronize(st));
+    stream_wait(c.name, st);
     if (overlap) {
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
-        HIPCHK(c.name, hipStreamSynchronize(st));
+        stream_wait(c.name, st);
     }
 }
 
@@ -639,7 +672,7 @@ void run_staged(const Call &c, StageSet &S)
                                       hipMemcpyHostToDevice, S.st_in));
         HIPCHK(c.name, hipEventRecord(S.ev_in[ch & 1], S.st_in));
     };
-    HIPCHK(c.name, hipDeviceSynchronize());
+    entry_sync(c.name);
     h2d(0);
     for (size_t ch = 0; ch < nchunks; ch++) {
         const int sl = (int) (ch & 1);
@@ -672,13 +705,13 @@ void run_staged(const Call &c, StageSet &S)
                                                  S.st_c);
             if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
         }
-        HIPCHK(c.name, hipStreamSynchronize(S.st_c));
+        stream_wait(c.name, S.st_c);
         barrier(c);  // every shard of my out[sl] written
         HIPCHK(c.name, hipMemcpyAsync(result + ch * C * s, S.out(idx, sl), n * s,
                                       hipMemcpyDeviceToHost, S.st_out));
         HIPCHK(c.name, hipEventRecord(S.ev_out[sl], S.st_out));
     }
-    HIPCHK(c.name, hipStreamSynchronize(S.st_out));
+    stream_wait(c.name, S.st_out);
     if (overlap) {
         memcpy(c.target, result, c.nbytes);
         free(result);
@@ -738,7 +771,7 @@ void run_host(const Call &c)
         if (e != hipSuccess) fatal(c.name, "combine launch: %s", hipGetErrorString(e));
         char *hout = hbuf + (size_t) P * cb;
         HIPCHK(c.name, hipMemcpyAsync(hout, dout, nb, hipMemcpyDeviceToHost, st));
-        HIPCHK(c.name, hipStreamSynchronize(st));
+        stream_wait(c.name, st);
         memcpy(result + off * s, hout, nb);
     }
     barrier(c);  // src/reductions.c:113

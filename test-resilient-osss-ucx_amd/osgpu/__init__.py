@@ -76,6 +76,15 @@ def load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() "
                            "(the reduction has no CPU implementation)")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64 (same
+    # SONAME libamdhip64.so.7, different file name).  Loaded first, our
+    # NEEDED entry binds to torch's copy; loaded after us, torch would map a
+    # second runtime next to /opt/rocm's and the two corrupt each other's
+    # heap at exit.  So when torch is importable, it goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     for name in ENTRY_POINTS:

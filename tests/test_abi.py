@@ -92,6 +92,22 @@ int main(void){
     assert r.stdout.strip() == "4"
 
 
+def test_single_hip_runtime_in_process():
+    """Loading the library and torch in either order maps exactly one
+    libamdhip64 (two runtimes in one process corrupt the heap at exit)."""
+    code = (
+        "import sys; sys.path[:0]=[%r]\n"
+        "import osgpu; osgpu.load()\n"
+        "import torch\n"
+        "maps = open('/proc/self/maps').read().split('\\n')\n"
+        "print(len({l.split()[-1] for l in maps if 'libamdhip64' in l}))\n"
+    ) % os.path.join(ROOT, "test-resilient-osss-ucx_amd")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == "1"
+
+
 def test_has_op_matches_reference_table(lib):
     import oracle as O
     for ti, t in enumerate(O.TYPES):

@@ -20,9 +20,13 @@ from support import team as T  # noqa: E402
 sig = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
        ctypes.c_int, ctypes.c_int]
 out = {}
-for n in (1024, 65536, 1 << 20):
+mode = os.environ.get("PROBE_TAG", "")
+KINDS = [k == "1" for k in os.environ.get("PROBE_KINDS", "10").split(",")] if os.environ.get("PROBE_KINDS") else (True, False)
+FIN = os.environ.get("PROBE_FINALIZE", "1") == "1"
+SIZES = [int(x) for x in os.environ.get("PROBE_SIZES", "1024,65536,1048576").split(",")]
+for n in SIZES:
     row = {}
-    for device in (True, False):
+    for device in KINDS:
         tm = T.Team(2, 2 * n * 4 + 8192, device=device)
         tm.pet.pet_time_to_all.restype = ctypes.c_double
         tm.pet.pet_time_to_all.argtypes = sig
@@ -31,16 +35,22 @@ for n in (1024, 65536, 1 << 20):
         tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
         src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
         if device:
-            for name, path in (("team", osgpu.PATH_AUTO), ("pull", osgpu.PATH_PULL)):
+            paths = (("team", osgpu.PATH_AUTO), ("pull", osgpu.PATH_PULL))
+            sel = os.environ.get("PROBE_PATHS")
+            if sel:
+                paths = [p for p in paths if p[0] in sel.split(",")]
+            for name, path in paths:
                 tm.lib.osgpu_set_path(path)
-                row[name + "_us"] = tm.pet.pet_time_to_all(fn, 2, tgt, src, None, n, 200) * 1e6
+                row[name + "_us"] = tm.pet.pet_time_to_all(
+                    fn, 2, tgt, src, None, n, int(os.environ.get("PROBE_REPS", "200"))) * 1e6
             tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
         else:
             ps = (ctypes.c_void_p * 2)(tm.ptr(0, tm.psync_off), tm.ptr(1, tm.psync_off))
             row["host_staged_us"] = tm.pet.pet_time_to_all(fn, 2, tgt, src, ps, n, 200) * 1e6
-        tm.lib.osgpu_finalize()
+        if FIN:
+            tm.lib.osgpu_finalize()
         del tm
     srcs = O.team_inputs("int", 2, n, 5, "bits")
     row["cpu_reference_loop_us"] = O.cpu_baseline("int", "sum", srcs, reps=200, pin=True) * 1e6
     out[n] = row
-    print(json.dumps({"nreduce": n, **row}), flush=True)
+    print(json.dumps({"tag": mode, "nreduce": n, **row}), flush=True)
