@@ -39,6 +39,18 @@ hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *c
 hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,
                                   size_t n, hipStream_t s);
 
+// Byte copy of up to kMaxCopySegs independent ranges in one launch (copy.hip):
+// the data movement of broadcast / collect / fcollect / alltoall.  Sources may
+// be peer HBM.  Zero-length segments are skipped; more than kMaxCopySegs
+// non-empty segments is an error (callers batch).
+constexpr int kMaxCopySegs = 8;
+struct CopySeg {
+    const void *src;
+    void *dst;
+    size_t bytes;
+};
+hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
+
 // x87 80-bit extended combine (soft-float on the GPU), longdouble.hip
 hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, size_t n,
                              hipStream_t s);

@@ -1,0 +1,134 @@
+// copy.hip -- the data-movement kernel of the broadcast / collect / fcollect /
+// alltoall collectives (shmem_collect.cpp): up to kMaxCopySegs independent
+// byte ranges (src -> dst), each source in local HBM or in a peer GPU's HBM
+// mapped into this process, copied by ONE launch.
+//
+// The reference moves these bytes with shmemc_put / shmemc_get over UCX
+// (src/shmemc/fcollect.c:29-35, src/shmemc/collect.c:57-66,
+// src/shmemc/broadcast.c:39-41).  Here the owner of every target pulls all
+// its pieces with 16-byte streaming loads: HBM-bound on one GPU, xGMI-bound
+// across GPUs; 2 bytes of traffic (read + write) per byte copied.
+//
+// Layout of a launch: each segment gets ceil(body / (256 * U)) workgroups of
+// 256 lanes, each lane U 16-byte vectors (all loads issued before the first
+// store, non-temporal both ways -- the shape tools/tune_combine.hip found
+// fastest for the combine).  Vectors are aligned on the DESTINATION; the
+// source may sit at any 4-byte phase (gfx950 serves dword-aligned
+// global_load_dwordx4), so a 32-bit collect whose block offsets are not
+// 16-byte multiples stays on the vector path.  The first workgroup of a
+// segment also copies the unaligned head (< 16 B) and tail (< 16 B) bytes.
+// A segment whose source and destination differ in byte phase (impossible for
+// 32/64-bit elements at natural alignment) takes the byte kernel.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "combine.hpp"
+
+namespace osgpu {
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B load
+
+constexpr int kThreads = 256;
+constexpr int kU = 4;  // 16-B vectors per lane
+constexpr size_t kBlockBytes = (size_t) kThreads * kU * 16;
+
+struct SegTable {
+    const char *src[kMaxCopySegs];
+    char *dst[kMaxCopySegs];
+    size_t bytes[kMaxCopySegs];
+    unsigned first_block[kMaxCopySegs + 1];
+    int n;
+};
+
+__device__ __forceinline__ int find_seg(const SegTable &t, unsigned b)
+{
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxCopySegs; i++)
+        if (i < t.n && b >= t.first_block[i]) k = i;
+    return k;
+}
+
+__global__ __launch_bounds__(kThreads) void copy_vec_kernel(SegTable t)
+{
+    const int k = find_seg(t, blockIdx.x);
+    const char *s = t.src[k];
+    char *d = t.dst[k];
+    const size_t bytes = t.bytes[k];
+    size_t head = (size_t) ((0 - (uintptr_t) d) & 15);
+    if (head > bytes) head = bytes;
+    const size_t nvec = (bytes - head) / 16;
+    const size_t tail0 = head + nvec * 16;
+    const unsigned lb = blockIdx.x - t.first_block[k];
+    if (lb == 0) {
+        const unsigned x = threadIdx.x;
+        if (x < head) d[x] = s[x];
+        if (x < bytes - tail0) d[tail0 + x] = s[tail0 + x];
+    }
+    const u32x4_a4 *sv = reinterpret_cast<const u32x4_a4 *>(s + head);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(d + head);
+    const size_t base = (size_t) lb * kThreads * kU + threadIdx.x;
+    u32x4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const size_t i = base + (size_t) u * kThreads;
+        if (i < nvec) v[u] = __builtin_nontemporal_load(sv + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const size_t i = base + (size_t) u * kThreads;
+        if (i < nvec) __builtin_nontemporal_store(v[u], dv + i);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void copy_byte_kernel(SegTable t)
+{
+    const int k = find_seg(t, blockIdx.x);
+    const size_t per_block = (size_t) kThreads * 16;
+    const size_t lo = (size_t) (blockIdx.x - t.first_block[k]) * per_block;
+    for (size_t i = lo + threadIdx.x; i < t.bytes[k] && i < lo + per_block; i += kThreads)
+        t.dst[k][i] = t.src[k][i];
+}
+
+}  // namespace
+
+hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t stream)
+{
+    SegTable vt{}, bt{};
+    unsigned vblocks = 0, bblocks = 0;
+    for (int i = 0; i < nseg; i++) {
+        const CopySeg &g = segs[i];
+        if (g.bytes == 0) continue;
+        const uintptr_t phase = (uintptr_t) g.src ^ (uintptr_t) g.dst;
+        SegTable &t = (phase & 3) ? bt : vt;
+        unsigned &nb = (phase & 3) ? bblocks : vblocks;
+        const size_t per = (phase & 3) ? (size_t) kThreads * 16 : kBlockBytes;
+        const size_t blocks = (g.bytes + per - 1) / per;
+        if (blocks > 0x7fffffffu - nb) return hipErrorInvalidValue;
+        if (t.n == kMaxCopySegs) return hipErrorInvalidValue;  // callers batch
+        t.src[t.n] = (const char *) g.src;
+        t.dst[t.n] = (char *) g.dst;
+        t.bytes[t.n] = g.bytes;
+        t.first_block[t.n] = nb;
+        t.n++;
+        nb += (unsigned) blocks;
+    }
+    if (vt.n) {
+        vt.first_block[vt.n] = vblocks;
+        hipLaunchKernelGGL(copy_vec_kernel, dim3(vblocks), dim3(kThreads), 0, stream, vt);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (bt.n) {
+        bt.first_block[bt.n] = bblocks;
+        hipLaunchKernelGGL(copy_byte_kernel, dim3(bblocks), dim3(kThreads), 0, stream, bt);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace osgpu

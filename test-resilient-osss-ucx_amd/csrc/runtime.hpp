@@ -1,0 +1,143 @@
+// runtime.hpp -- internal services shared by the collectives of
+// libosgpu_reduce.so (runtime.cpp): error reporting, stream completion, the
+// OpenSHMEM PE services the library borrows from the application's runtime,
+// the device symmetric-heap registry, per-PE streams/scratch, the RCCL
+// communicator, and the host-staging sets of the STAGED paths.
+// Not installed: the public surface is include/osgpu_reduce.h.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <stdio.h>
+#include <unistd.h>
+
+#include <vector>
+
+namespace osgpu {
+namespace rt {
+
+// ------------------------------------------------------------------ errors
+
+void set_err(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+[[noreturn]] void fatal(const char *where, const char *fmt, ...)
+    __attribute__((format(printf, 2, 3)));
+int debug_level();
+
+// OSGPU_DEBUG=1: one stderr line per protocol step (call entry, path,
+// barriers, launches, syncs) -- for diagnosing multi-process runs
+#define DBG(...)                                                               \
+    do {                                                                       \
+        if (::osgpu::rt::debug_level() > 0) {                                  \
+            fprintf(stderr, "[osgpu pid %d] ", (int) getpid());                \
+            fprintf(stderr, __VA_ARGS__);                                      \
+            fputc('\n', stderr);                                               \
+            fflush(stderr);                                                    \
+        }                                                                      \
+    } while (0)
+
+#define HIPCHK(where, call)                                                    \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess)                                                  \
+            ::osgpu::rt::fatal(where, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+// ----------------------------------------------------------- synchronisation
+
+int env_choice(const char *var, const char *alt, int def_is_alt);
+void entry_sync(const char *where);
+void stream_wait(const char *where, hipStream_t st);
+
+// --------------------------------------------------------------- type info
+
+size_t type_size(int t);
+bool has_op(int t, int op);
+
+// ------------------------------------------------------------- PE services
+
+struct PeOps {
+    int (*my_pe)(void) = nullptr;
+    int (*n_pes)(void) = nullptr;
+    void (*barrier)(int, int, int, long *) = nullptr;
+    void (*getmem)(void *, const void *, size_t, int) = nullptr;
+};
+PeOps pe_ops();
+
+// -------------------------------------------------------- device sym. heap
+
+struct HeapEntry {
+    char *base = nullptr;
+    size_t bytes = 0;
+};
+bool heap_segment(int pe, int seg, HeapEntry *out);
+bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off);
+bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out);
+
+// ---------------------------------------------------------------- RCCL
+
+struct Rccl {
+    ncclComm_t world = nullptr;
+    int npes = 0, me = -1;
+};
+extern Rccl g_rccl;
+int path_mode();
+
+// ------------------------------------------------------ per-PE / per-thread
+
+hipStream_t thread_stream(const char *where);
+hipStream_t pe_stream(const char *where, int me);
+void *device_scratch(const char *where, int me, size_t bytes);
+void *host_stage(const char *where, int me, size_t bytes);
+
+enum MemKind { MEM_HOST = 0, MEM_DEVICE = 1 };
+MemKind mem_kind(const void *p, int *dev);
+bool ranges_overlap(const void *a, const void *b, size_t n);
+void fold_order(int me, int PE_start, int step, int PE_size, int *order);
+
+// ------------------------------------------------------------ active sets
+
+// One collective call on an active set (PE_start, 2^logPE_stride, PE_size).
+struct Coll {
+    const char *name = nullptr;
+    int PE_start = 0, logPE_stride = 0, PE_size = 0;
+    long *pSync = nullptr;
+    int me = -1, step = 1;
+    PeOps ops;
+    // index of PE `pe` in the active set, or -1
+    int index_of(int pe) const
+    {
+        if (pe < PE_start || (pe - PE_start) % step) return -1;
+        const int i = (pe - PE_start) / step;
+        return i < PE_size ? i : -1;
+    }
+    int pe_at(int i) const { return PE_start + i * step; }
+};
+
+// Fills name/active set/pSync/me/ops; aborts on an invalid active set or a
+// missing runtime (the shared entry checks of every collective).
+Coll make_coll(const char *name, int PE_start, int logPE_stride, int PE_size, long *pSync);
+
+void barrier(const Coll &c);
+
+// ---------------------------------------------------------- host staging
+
+// Device staging of one PE for one active set: four slots of `slot` bytes,
+// mapped into every member PE (same process: raw pointer; other processes:
+// HIP IPC), exchanged once through spare pSync words (runtime.cpp).
+struct StageSet {
+    bool ok = false;
+    int device = -1;
+    size_t slot = 0;                 // bytes per slot (in0, in1, out0, out1)
+    char *local = nullptr;
+    std::vector<char *> peer;        // by active-set index
+    std::vector<void *> opened;      // IPC mappings to close
+    hipStream_t st_in = nullptr, st_c = nullptr, st_out = nullptr;
+    hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+    char *in(int i, int s) const { return peer[i] + (size_t) s * slot; }
+    char *out(int i, int s) const { return peer[i] + (size_t) (2 + s) * slot; }
+    char *region(int i) const { return peer[i]; }  // the whole 4-slot area
+};
+StageSet *stage_setup(const Coll &c);
+
+}  // namespace rt
+}  // namespace osgpu

@@ -1,0 +1,448 @@
+// shmem_collect.cpp -- the data-movement collectives on the reduce path's
+// machinery: broadcast32/64, collect32/64,
+// fcollect32/64, alltoall32/64, same signatures as the reference
+// (include/shmem/api.h:2415-2450).
+//
+// Reference algorithms (bytes move with UCX puts/gets, one PE at a time):
+//   broadcast  src/shmemc/broadcast.c:29-42 (linear: barrier, every non-root
+//              gets the root's source; the tree/binomial variants :48-250
+//              forward it) -- the root's own target is never written;
+//   collect    src/shmemc/collect.c:28-70: an offset wavefront through pSync
+//              (each PE learns the sum of its left neighbours' nelems), then
+//              every PE puts its source at that offset of every target,
+//              barrier;
+//   fcollect   src/shmemc/fcollect.c:25-38: every PE puts its source at
+//              block vpe = (me - PE_start) >> logPE_stride of every target,
+//              barrier;
+//   alltoall   src/alltoall.c:61-84: block i of my target <- a block of PE
+//              i's source (gets, no synchronisation at all).
+//
+// Here every PE PULLS all the pieces of its own target in one launch of
+// copy.hip's kernel (16-byte streaming loads from local or peer HBM):
+//
+//   COPY    device-resident, source symmetric in registered heaps (any
+//           active-set size): copy kernel over peer pointers, two barriers
+//           (sources ready / every reader done);
+//   RCCL    device-resident without registered heaps, one process per GPU,
+//           whole job: ncclBroadcast / ncclAllGather (broadcast, fcollect);
+//   STAGED  host arguments: H2D my source -> copy kernel over every PE's
+//           IPC-mapped device staging -> D2H of my target, chunked;
+//   GETMEM  host arguments when staging cannot be mapped: the reference's
+//           own linear algorithm over the runtime's shmem_getmem.
+//
+// collect needs every PE's nelems before any byte moves: each PE publishes
+// it in a spare pSync word (the reference's barrier uses pSync[0] only,
+// src/shmemc/barrier.c:64-97), reads its peers' with shmem_getmem after the
+// first barrier and clears its word after the last -- pSync is returned at
+// SHMEM_SYNC_VALUE, as the reference's wavefront leaves it (collect.c:68).
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/osgpu_reduce.h"
+#include "combine.hpp"
+#include "runtime.hpp"
+
+namespace {
+
+using namespace osgpu::rt;
+
+enum Kind { K_BCAST, K_COLLECT, K_FCOLLECT, K_ALLTOALL };
+
+constexpr int kCountWord = 8;  // pSync word carrying nelems during collect
+
+// one piece of my target: bytes [src_off, src_off + len) of the source of the
+// PE at active-set index `from`, to byte dst_off of my target
+struct Piece {
+    int from;
+    size_t src_off, len, dst_off;
+};
+
+struct CCall : Coll {
+    Kind kind = K_BCAST;
+    void *target = nullptr;
+    const void *source = nullptr;
+    size_t esz = 0;
+    size_t nelems = 0;
+    int root = 0;                  // broadcast: active-set index of the root
+    int idx = -1;                  // my active-set index
+    std::vector<size_t> src_len;   // bytes of every member's source
+    std::vector<Piece> pieces;     // what my target receives
+    size_t out_bytes = 0;          // extent of my target that is written
+};
+
+bool overlap2(const void *a, size_t na, const void *b, size_t nb)
+{
+    if (!na || !nb) return false;
+    const uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
+    return x < y + nb && y < x + na;
+}
+
+// Every member's nelems (collect), through pSync[kCountWord] + getmem.
+void exchange_counts(CCall &c)
+{
+    if (!c.ops.getmem) fatal(c.name, "collect needs shmem_getmem to learn every PE's nelems");
+    if (mem_kind(c.pSync, nullptr) != MEM_HOST)
+        fatal(c.name, "collect needs pSync in host symmetric memory");
+    c.pSync[kCountWord] = (long) c.nelems;
+    barrier(c);  // every count published (and, for the data, every source ready)
+    c.src_len.assign(c.PE_size, 0);
+    for (int i = 0; i < c.PE_size; i++) {
+        long n = 0;
+        if (i == c.idx) n = (long) c.nelems;
+        else c.ops.getmem(&n, &c.pSync[kCountWord], sizeof(long), c.pe_at(i));
+        if (n < 0) fatal(c.name, "negative nelems published by PE %d", c.pe_at(i));
+        c.src_len[i] = (size_t) n * c.esz;
+    }
+}
+
+// The pieces of my target and every member's source extent.
+void plan(CCall &c)
+{
+    const int P = c.PE_size;
+    const size_t nb = c.nelems * c.esz;
+    c.pieces.clear();
+    switch (c.kind) {
+    case K_BCAST:
+        c.src_len.assign(P, 0);
+        c.src_len[c.root] = nb;
+        if (c.idx != c.root) c.pieces.push_back({c.root, 0, nb, 0});
+        c.out_bytes = c.idx != c.root ? nb : 0;
+        break;
+    case K_FCOLLECT:
+        c.src_len.assign(P, nb);
+        for (int i = 0; i < P; i++) c.pieces.push_back({i, 0, nb, (size_t) i * nb});
+        c.out_bytes = (size_t) P * nb;
+        break;
+    case K_COLLECT: {  // src_len from exchange_counts
+        size_t off = 0;
+        for (int i = 0; i < P; i++) {
+            c.pieces.push_back({i, 0, c.src_len[i], off});
+            off += c.src_len[i];
+        }
+        c.out_bytes = off;
+        break;
+    }
+    case K_ALLTOALL:
+        c.src_len.assign(P, (size_t) P * nb);
+        for (int i = 0; i < P; i++)
+            c.pieces.push_back({i, (size_t) c.idx * nb, nb, (size_t) i * nb});
+        c.out_bytes = (size_t) P * nb;
+        break;
+    }
+}
+
+// Does any PE (me included) read my source while my target is written?
+bool my_source_read(const CCall &c)
+{
+    if (c.kind == K_BCAST) return c.idx == c.root;  // the root's target is untouched anyway
+    return true;
+}
+
+void copy_pieces(const CCall &c, const std::vector<osgpu::CopySeg> &segs, hipStream_t st)
+{
+    for (size_t i = 0; i < segs.size(); i += osgpu::kMaxCopySegs) {
+        const int n = (int) std::min(segs.size() - i, (size_t) osgpu::kMaxCopySegs);
+        hipError_t e = osgpu::launch_copy(segs.data() + i, n, st);
+        if (e != hipSuccess) fatal(c.name, "copy launch: %s", hipGetErrorString(e));
+    }
+}
+
+// ------------------------------------------------------------ COPY (device)
+
+// Peer addresses of every member's source (symmetric: same segment and
+// offset in every registered heap); false if the heaps do not cover them.
+bool device_sources(const CCall &c, std::vector<const char *> &src)
+{
+    size_t mine = c.src_len[c.idx];
+    int seg = -1;
+    size_t off = 0;
+    // locate the source object in my heap (at least one byte, so that a
+    // zero-length contribution still has a segment)
+    if (!heap_locate(c.me, c.source, mine ? mine : 1, &seg, &off)) return false;
+    src.assign(c.PE_size, nullptr);
+    for (int i = 0; i < c.PE_size; i++) {
+        bool needed = false;
+        for (const Piece &p : c.pieces) needed |= (p.from == i && p.len);
+        if (!needed) continue;
+        char *p = nullptr;
+        if (!heap_peer(c.pe_at(i), seg, off, c.src_len[i], &p)) return false;
+        src[i] = p;
+    }
+    return true;
+}
+
+void run_copy(const CCall &c, const std::vector<const char *> &src, bool counts_done)
+{
+    hipStream_t st = pe_stream(c.name, c.me);
+    const bool scratch = my_source_read(c) &&
+                         overlap2(c.target, c.out_bytes, c.source, c.src_len[c.idx]);
+    char *out = scratch ? (char *) device_scratch(c.name, c.me, c.out_bytes) : (char *) c.target;
+    std::vector<osgpu::CopySeg> segs;
+    for (const Piece &p : c.pieces)
+        if (p.len) segs.push_back({src[p.from] + p.src_off, out + p.dst_off, p.len});
+    DBG("%s PE %d: copy path, %zu pieces, %zu bytes out%s", c.name, c.me, segs.size(),
+        c.out_bytes, scratch ? " (scratch)" : "");
+    if (!counts_done) {
+        entry_sync(c.name);
+        barrier(c);  // every source ready
+    }
+    copy_pieces(c, segs, st);
+    stream_wait(c.name, st);
+    barrier(c);  // every reader of my source is done
+    if (scratch && c.out_bytes) {
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.out_bytes, hipMemcpyDeviceToDevice, st));
+        stream_wait(c.name, st);
+    }
+}
+
+// ------------------------------------------------------------ RCCL (device)
+
+bool rccl_whole_job(const CCall &c)
+{
+    return g_rccl.world && c.PE_start == 0 && c.step == 1 && c.PE_size == g_rccl.npes &&
+           c.me == g_rccl.me && (c.kind == K_BCAST || c.kind == K_FCOLLECT);
+}
+
+void run_rccl(const CCall &c)
+{
+    hipStream_t st = pe_stream(c.name, c.me);
+    const size_t nb = c.nelems * c.esz;
+    entry_sync(c.name);
+    ncclResult_t r;
+    if (c.kind == K_BCAST) {
+        // the root receives in place (recvbuff == sendbuff: RCCL copies
+        // nothing), so its target stays untouched as in the reference
+        void *recv = c.idx == c.root ? (void *) c.source : c.target;
+        r = ncclBroadcast(c.source, recv, nb, ncclUint8, c.root, g_rccl.world, st);
+        if (r != ncclSuccess) fatal(c.name, "ncclBroadcast: %s", ncclGetErrorString(r));
+        stream_wait(c.name, st);
+        return;
+    }
+    const bool scratch = overlap2(c.target, c.out_bytes, c.source, nb) &&
+                         (char *) c.target + (size_t) c.idx * nb != (const char *) c.source;
+    char *out = scratch ? (char *) device_scratch(c.name, c.me, c.out_bytes) : (char *) c.target;
+    r = ncclAllGather(c.source, out, nb, ncclUint8, g_rccl.world, st);
+    if (r != ncclSuccess) fatal(c.name, "ncclAllGather: %s", ncclGetErrorString(r));
+    stream_wait(c.name, st);
+    if (scratch) {
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.out_bytes, hipMemcpyDeviceToDevice, st));
+        stream_wait(c.name, st);
+    }
+}
+
+// ------------------------------------------------------------ STAGED (host)
+
+// Chunk k covers source bytes [k*C, (k+1)*C) of every member.  Each PE
+// stages its chunk in the `in` area of its device staging; each PE's copy
+// kernel pulls the parts of its pieces inside chunk k from the members' `in`
+// areas (IPC-mapped) into its own `out` area; D2H to the target.  The four
+// slots of a StageSet are one region: in = C bytes, out = P*C bytes.
+void run_staged(const CCall &c, StageSet &S)
+{
+    const int P = c.PE_size;
+    const size_t region = 4 * S.slot;
+    size_t C = region / (size_t) (P + 1);
+    C &= ~(size_t) 255;
+    if (C == 0) fatal(c.name, "staging too small for %d PEs", P);
+    size_t maxlen = 0;
+    for (size_t l : c.src_len) maxlen = std::max(maxlen, l);
+    const size_t nchunks = (maxlen + C - 1) / C;
+    const size_t mine = c.src_len[c.idx];
+    const bool tmp = overlap2(c.target, c.out_bytes, c.source, mine);
+    char *result = tmp ? (char *) malloc(c.out_bytes) : (char *) c.target;
+    if (tmp && !result) fatal(c.name, "out of memory for the temporary target");
+    char *in_me = S.region(c.idx);
+    char *out_me = S.region(c.idx) + C;
+    std::vector<osgpu::CopySeg> segs;
+    std::vector<size_t> seg_dst;  // target offset of each staged piece part
+
+    entry_sync(c.name);
+    for (size_t k = 0; k < nchunks; k++) {
+        const size_t lo = k * C, hi = lo + C;
+        if (mine > lo) {
+            const size_t n = std::min(mine, hi) - lo;
+            HIPCHK(c.name, hipMemcpyAsync(in_me, (const char *) c.source + lo, n,
+                                          hipMemcpyHostToDevice, S.st_in));
+            stream_wait(c.name, S.st_in);
+        }
+        barrier(c);  // chunk k staged everywhere; every `in` area of k-1 drained
+        segs.clear();
+        seg_dst.clear();
+        size_t packed = 0;
+        for (const Piece &p : c.pieces) {
+            const size_t a = std::max(p.src_off, lo), b = std::min(p.src_off + p.len, hi);
+            if (a >= b) continue;
+            segs.push_back({S.region(p.from) + (a - lo), out_me + packed, b - a});
+            seg_dst.push_back(p.dst_off + (a - p.src_off));
+            packed += b - a;
+        }
+        copy_pieces(c, segs, S.st_c);
+        stream_wait(c.name, S.st_c);
+        barrier(c);  // every reader of chunk k is done
+        for (size_t i = 0; i < segs.size(); i++)
+            HIPCHK(c.name, hipMemcpyAsync(result + seg_dst[i], segs[i].dst, segs[i].bytes,
+                                          hipMemcpyDeviceToHost, S.st_out));
+        stream_wait(c.name, S.st_out);
+    }
+    if (tmp) {
+        memcpy(c.target, result, c.out_bytes);
+        free(result);
+    }
+}
+
+// GETMEM: the reference's linear schedule over the runtime's getmem (used
+// only when the staging cannot be mapped by every PE).  No arithmetic is
+// involved, so nothing is left for the GPU to do on this path.
+void run_getmem(const CCall &c)
+{
+    if (!c.ops.getmem) fatal(c.name, "host-memory arguments need shmem_getmem");
+    const bool tmp = overlap2(c.target, c.out_bytes, c.source, c.src_len[c.idx]) &&
+                     my_source_read(c);
+    char *result = tmp ? (char *) malloc(c.out_bytes) : (char *) c.target;
+    if (tmp && !result) fatal(c.name, "out of memory for the temporary target");
+    for (const Piece &p : c.pieces) {
+        if (!p.len) continue;
+        const char *s = (const char *) c.source + p.src_off;
+        if (p.from == c.idx) memmove(result + p.dst_off, s, p.len);
+        else c.ops.getmem(result + p.dst_off, s, p.len, c.pe_at(p.from));
+    }
+    barrier(c);  // every reader of my source is done
+    if (tmp) {
+        memcpy(c.target, result, c.out_bytes);
+        free(result);
+    }
+}
+
+// ------------------------------------------------------------ dispatcher
+
+void collective(const char *name, Kind kind, size_t esz, void *target, const void *source,
+                size_t nelems, int PE_root, int PE_start, int logPE_stride, int PE_size,
+                long *pSync)
+{
+    CCall c;
+    static_cast<Coll &>(c) = make_coll(name, PE_start, logPE_stride, PE_size, pSync);
+    c.kind = kind;
+    c.target = target;
+    c.source = source;
+    c.esz = esz;
+    c.nelems = nelems;
+    c.root = PE_root;
+    c.idx = c.index_of(c.me);
+    if (c.idx < 0) fatal(name, "PE %d is not in the active set", c.me);
+    if (kind == K_BCAST && (PE_root < 0 || PE_root >= PE_size))
+        fatal(name, "PE_root %d outside the active set of %d PEs", PE_root, PE_size);
+    if (kind != K_COLLECT && nelems == 0) {  // nothing moves; the collective still syncs
+        barrier(c);
+        barrier(c);
+        return;
+    }
+    int dt = -1, ds = -1;
+    const MemKind kt = mem_kind(target, &dt), ks = mem_kind(source, &ds);
+    if (kt != ks) fatal(name, "target and source must both be device or both be host memory");
+
+    bool counts_done = false;
+    if (kind == K_COLLECT) {
+        if (kt == MEM_DEVICE) entry_sync(name);  // my source is final before I publish
+        exchange_counts(c);                      // includes the first barrier
+        counts_done = true;
+    }
+    plan(c);
+    size_t moved = 0;
+    for (size_t l : c.src_len) moved += l;
+    if (moved == 0) {  // a collect of empty contributions only synchronises
+        barrier(c);
+        c.pSync[kCountWord] = 0;
+        return;
+    }
+
+    if (kt == MEM_HOST) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+            fatal(name, "no GPU visible: the collectives run on the GPU");
+        if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
+        const char *hp = getenv("OSGPU_HOST_PATH");
+        const bool getmem_only = hp && !strcmp(hp, "getmem");
+        if (!counts_done) barrier(c);  // sources ready (staging setup runs after it)
+        StageSet *S = getmem_only ? nullptr : stage_setup(c);
+        if (S) run_staged(c, *S);
+        else run_getmem(c);
+        barrier(c);
+        if (kind == K_COLLECT) c.pSync[kCountWord] = 0;
+        return;
+    }
+
+    int cur = 0;
+    HIPCHK(name, hipGetDevice(&cur));
+    if (cur != dt) HIPCHK(name, hipSetDevice(dt));
+    const int mode = path_mode();
+    std::vector<const char *> src;
+    if (mode != OSGPU_PATH_RCCL && device_sources(c, src)) {
+        run_copy(c, src, counts_done);
+    } else if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_RCCL) && !counts_done &&
+               rccl_whole_job(c)) {
+        run_rccl(c);
+    } else {
+        fatal(name,
+              "device-resident arguments need every active PE's device heap registered "
+              "(osgpu_heap_register)%s",
+              kind == K_BCAST || kind == K_FCOLLECT
+                  ? " or an RCCL communicator over the whole job"
+                  : "");
+    }
+    if (kind == K_COLLECT) c.pSync[kCountWord] = 0;
+    if (cur != dt) HIPCHK(name, hipSetDevice(cur));
+}
+
+}  // namespace
+
+// pshmem_* strong, shmem_* weak aliases (as src/broadcast.c:14-20,
+// src/collect.c:14-20, src/fcollect.c:14-20, src/alltoall.c:11-23 under
+// ENABLE_PSHMEM)
+#define OSGPU_ALIAS(_n) __attribute__((weak, alias("pshmem_" #_n)))
+
+#define OSGPU_DEFINE_COLL(_bits, _bytes)                                                   \
+    extern "C" void pshmem_broadcast##_bits(void *target, const void *source, size_t nelems, \
+                                            int PE_root, int PE_start, int logPE_stride,   \
+                                            int PE_size, long *pSync)                      \
+    {                                                                                      \
+        collective("shmem_broadcast" #_bits, K_BCAST, _bytes, target, source, nelems,      \
+                   PE_root, PE_start, logPE_stride, PE_size, pSync);                       \
+    }                                                                                      \
+    extern "C" void shmem_broadcast##_bits(void *, const void *, size_t, int, int, int,    \
+                                           int, long *) OSGPU_ALIAS(broadcast##_bits);     \
+    extern "C" void pshmem_collect##_bits(void *target, const void *source, size_t nelems, \
+                                          int PE_start, int logPE_stride, int PE_size,     \
+                                          long *pSync)                                     \
+    {                                                                                      \
+        collective("shmem_collect" #_bits, K_COLLECT, _bytes, target, source, nelems, 0,   \
+                   PE_start, logPE_stride, PE_size, pSync);                                \
+    }                                                                                      \
+    extern "C" void shmem_collect##_bits(void *, const void *, size_t, int, int, int,      \
+                                         long *) OSGPU_ALIAS(collect##_bits);              \
+    extern "C" void pshmem_fcollect##_bits(void *target, const void *source, size_t nelems, \
+                                           int PE_start, int logPE_stride, int PE_size,    \
+                                           long *pSync)                                    \
+    {                                                                                      \
+        collective("shmem_fcollect" #_bits, K_FCOLLECT, _bytes, target, source, nelems, 0, \
+                   PE_start, logPE_stride, PE_size, pSync);                                \
+    }                                                                                      \
+    extern "C" void shmem_fcollect##_bits(void *, const void *, size_t, int, int, int,     \
+                                          long *) OSGPU_ALIAS(fcollect##_bits);            \
+    extern "C" void pshmem_alltoall##_bits(void *target, const void *source, size_t nelems, \
+                                           int PE_start, int logPE_stride, int PE_size,    \
+                                           long *pSync)                                    \
+    {                                                                                      \
+        collective("shmem_alltoall" #_bits, K_ALLTOALL, _bytes, target, source, nelems, 0, \
+                   PE_start, logPE_stride, PE_size, pSync);                                \
+    }                                                                                      \
+    extern "C" void shmem_alltoall##_bits(void *, const void *, size_t, int, int, int,     \
+                                          long *) OSGPU_ALIAS(alltoall##_bits);
+
+OSGPU_DEFINE_COLL(32, 4)
+OSGPU_DEFINE_COLL(64, 8)

@@ -26,373 +26,28 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
-#include <dlfcn.h>
-#include <stdarg.h>
-#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <unistd.h>
 
-#include <map>
-#include <mutex>
-#include <tuple>
 #include <vector>
 
 #include "../../include/osgpu_reduce.h"
 #include "combine.hpp"
+#include "runtime.hpp"
 
 namespace {
 
-// ------------------------------------------------------------------ errors
-
-thread_local char g_err[512];
-
-void set_err(const char *fmt, ...)
-{
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
-    va_end(ap);
-}
-
-// The shmem_* entry points are void (src/reductions.c:139-154); the
-// reference logs LOG_FATAL and returns on OOM (:55-61) and asserts on
-// transport errors (src/shmemc/comms.c:250).  Silent wrong results are
-// worse than both, so an unrecoverable error is reported and aborts.
-[[noreturn]] void fatal(const char *where, const char *fmt, ...)
-{
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    fprintf(stderr, "osgpu_reduce: %s: %s\n", where, buf);
-    fflush(stderr);
-    abort();
-}
-
-// OSGPU_DEBUG=1: one stderr line per protocol step (call entry, path,
-// barriers, launches, syncs) -- for diagnosing multi-process runs
-int debug_level()
-{
-    static int lvl = -1;
-    if (lvl < 0) {
-        const char *e = getenv("OSGPU_DEBUG");
-        lvl = e ? atoi(e) : 0;
-    }
-    return lvl;
-}
-
-#define DBG(...)                                                               \
-    do {                                                                       \
-        if (debug_level() > 0) {                                               \
-            fprintf(stderr, "[osgpu pid %d] ", (int) getpid());                \
-            fprintf(stderr, __VA_ARGS__);                                      \
-            fputc('\n', stderr);                                               \
-            fflush(stderr);                                                    \
-        }                                                                      \
-    } while (0)
-
-#define HIPCHK(where, call)                                                    \
-    do {                                                                       \
-        hipError_t e_ = (call);                                                \
-        if (e_ != hipSuccess) fatal(where, "%s: %s", #call, hipGetErrorString(e_)); \
-    } while (0)
-
-// ----------------------------------------------------------- synchronisation
-
-int env_choice(const char *var, const char *alt, int def_is_alt)
-{
-    const char *e = getenv(var);
-    if (!e) return def_is_alt;
-    return strcmp(e, alt) == 0;
-}
-
-// Entry: device work this process enqueued earlier (on any stream) may still
-// be producing `source`; the collective reads it only after it is done.
-// OSGPU_ENTRY_SYNC=none skips this for callers that synchronise themselves.
-void entry_sync(const char *where)
-{
-    static const int skip = env_choice("OSGPU_ENTRY_SYNC", "none", 0);
-    if (!skip) HIPCHK(where, hipDeviceSynchronize());
-}
-
-// Completion of our own stream: poll (default; the combine is short and the
-// wake-up latency of a blocking wait is a large share of a small call) or
-// block (OSGPU_SYNC=block).
-void stream_wait(const char *where, hipStream_t st)
-{
-    static const int block = env_choice("OSGPU_SYNC", "block", 0);
-    if (block) {
-        HIPCHK(where, hipStreamSynchronize(st));
-        return;
-    }
-    hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
-    if (e != hipSuccess) fatal(where, "stream: %s", hipGetErrorString(e));
-}
-
-// --------------------------------------------------------------- type info
-
-size_t type_size(int t)
-{
-    switch (t) {
-    case OSGPU_T_SHORT: return sizeof(short);
-    case OSGPU_T_INT: return sizeof(int);
-    case OSGPU_T_LONG: return sizeof(long);
-    case OSGPU_T_LONGLONG: return sizeof(long long);
-    case OSGPU_T_FLOAT: return sizeof(float);
-    case OSGPU_T_DOUBLE: return sizeof(double);
-    case OSGPU_T_LONGDOUBLE: return sizeof(long double);
-    case OSGPU_T_COMPLEXF: return 2 * sizeof(float);
-    case OSGPU_T_COMPLEXD: return 2 * sizeof(double);
-    }
-    return 0;
-}
-
-bool has_op(int t, int op)
-{
-    if (t < OSGPU_T_SHORT || t > OSGPU_T_COMPLEXD) return false;
-    switch (op) {
-    case OSGPU_OP_SUM: case OSGPU_OP_PROD: return true;
-    case OSGPU_OP_AND: case OSGPU_OP_OR: case OSGPU_OP_XOR: return t <= OSGPU_T_LONGLONG;
-    case OSGPU_OP_MAX: case OSGPU_OP_MIN: return t <= OSGPU_T_LONGDOUBLE;
-    }
-    return false;
-}
-
-// ------------------------------------------------------------- PE services
-
-struct PeOps {
-    int (*my_pe)(void) = nullptr;
-    int (*n_pes)(void) = nullptr;
-    void (*barrier)(int, int, int, long *) = nullptr;
-    void (*getmem)(void *, const void *, size_t, int) = nullptr;
-};
-
-std::mutex g_mu;
-PeOps g_ops;
-bool g_ops_set = false;
-
-PeOps pe_ops()
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ops_set) {
-        // bind to the OpenSHMEM runtime the application links (the reference
-        // library exports these as strong or weak symbols)
-        g_ops.my_pe = (int (*)(void)) dlsym(RTLD_DEFAULT, "shmem_my_pe");
-        g_ops.n_pes = (int (*)(void)) dlsym(RTLD_DEFAULT, "shmem_n_pes");
-        g_ops.barrier = (void (*)(int, int, int, long *)) dlsym(RTLD_DEFAULT, "shmem_barrier");
-        g_ops.getmem = (void (*)(void *, const void *, size_t, int)) dlsym(RTLD_DEFAULT,
-                                                                          "shmem_getmem");
-        g_ops_set = true;
-    }
-    return g_ops;
-}
-
-// -------------------------------------------------------- device sym. heap
-
-// A PE's device heap is one or more segments (separate allocations: HIP IPC
-// cannot export a single allocation of 2 GiB or more on this platform, see
-// DESIGN.md 6).  A symmetric object lives in the same segment at the same
-// offset on every PE.
-struct HeapEntry {
-    char *base = nullptr;
-    size_t bytes = 0;
-};
-std::vector<std::vector<HeapEntry>> g_heap;  // [PE][segment]
-
-bool heap_segment(int pe, int seg, HeapEntry *out)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (pe < 0 || (size_t) pe >= g_heap.size() || seg < 0 ||
-        (size_t) seg >= g_heap[pe].size() || !g_heap[pe][seg].base)
-        return false;
-    *out = g_heap[pe][seg];
-    return true;
-}
-
-// segment of PE `pe` holding [addr, addr + nbytes), and the offset in it
-bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (pe < 0 || (size_t) pe >= g_heap.size()) return false;
-    const char *p = (const char *) addr;
-    for (size_t s = 0; s < g_heap[pe].size(); s++) {
-        const HeapEntry &h = g_heap[pe][s];
-        if (h.base && p >= h.base && p + nbytes <= h.base + h.bytes) {
-            *seg = (int) s;
-            *off = (size_t) (p - h.base);
-            return true;
-        }
-    }
-    return false;
-}
-
-// address of the symmetric object at (seg, off) on PE pe, checked for nbytes
-bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out)
-{
-    HeapEntry h;
-    if (!heap_segment(pe, seg, &h) || off + nbytes > h.bytes) return false;
-    *out = h.base + off;
-    return true;
-}
-
-// ---------------------------------------------------------------- RCCL
-
-struct Rccl {
-    ncclComm_t world = nullptr;
-    int npes = 0, me = -1;
-} g_rccl;
-
-int g_path = -1;  // -1: not yet read from the environment
-
-int path_mode()
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_path < 0) {
-        g_path = OSGPU_PATH_AUTO;
-        const char *e = getenv("OSGPU_REDUCE_PATH");
-        if (e && !strcmp(e, "p2p")) g_path = OSGPU_PATH_P2P;
-        if (e && !strcmp(e, "rccl")) g_path = OSGPU_PATH_RCCL;
-        if (e && !strcmp(e, "pull")) g_path = OSGPU_PATH_PULL;
-    }
-    return g_path;
-}
-
-// ------------------------------------------------------ per-PE / per-thread
-
-// Resources of one PE on one device (stream, scratch, pinned staging).  Keyed
-// by (PE, device), not by thread: a PE is one logical thread of execution
-// whatever OS thread happens to make its calls, so nothing leaks when a
-// runtime runs PEs on short-lived threads.  Calls of one PE never overlap.
-struct PeCtx {
-    hipStream_t stream = nullptr;
-    void *dscratch = nullptr;
-    size_t dscratch_bytes = 0;
-    void *hstage = nullptr;  // pinned
-    size_t hstage_bytes = 0;
-};
-std::map<std::pair<int, int>, PeCtx *> g_pectx;
-
-// per-thread: the stream chosen with osgpu_set_stream (overrides the PE's),
-// and a default stream for the raw osgpu_combine launcher
-struct ThreadStream {
-    int device = -1;
-    hipStream_t stream = nullptr;
-    bool user_stream = false;
-};
-thread_local ThreadStream t_ctx;
-
-hipStream_t thread_stream(const char *where)
-{
-    int dev = 0;
-    HIPCHK(where, hipGetDevice(&dev));
-    if (t_ctx.stream && (t_ctx.user_stream || t_ctx.device == dev)) return t_ctx.stream;
-    HIPCHK(where, hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
-    t_ctx.device = dev;
-    t_ctx.user_stream = false;
-    return t_ctx.stream;
-}
-
-PeCtx &pe_ctx(const char *where, int me)
-{
-    int dev = 0;
-    HIPCHK(where, hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(g_mu);
-    PeCtx *&p = g_pectx[std::make_pair(me, dev)];
-    if (!p) {
-        p = new PeCtx();
-        HIPCHK(where, hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    }
-    return *p;
-}
-
-hipStream_t pe_stream(const char *where, int me)
-{
-    if (t_ctx.user_stream && t_ctx.stream) return t_ctx.stream;
-    return pe_ctx(where, me).stream;
-}
-
-void *device_scratch(const char *where, int me, size_t bytes)
-{
-    PeCtx &x = pe_ctx(where, me);
-    if (x.dscratch_bytes < bytes) {
-        if (x.dscratch) HIPCHK(where, hipFree(x.dscratch));
-        x.dscratch = nullptr;
-        x.dscratch_bytes = 0;
-        HIPCHK(where, hipMalloc(&x.dscratch, bytes));
-        x.dscratch_bytes = bytes;
-    }
-    return x.dscratch;
-}
-
-void *host_stage(const char *where, int me, size_t bytes)
-{
-    PeCtx &x = pe_ctx(where, me);
-    if (x.hstage_bytes < bytes) {
-        if (x.hstage) HIPCHK(where, hipHostFree(x.hstage));
-        x.hstage = nullptr;
-        x.hstage_bytes = 0;
-        HIPCHK(where, hipHostMalloc(&x.hstage, bytes, hipHostMallocDefault));
-        x.hstage_bytes = bytes;
-    }
-    return x.hstage;
-}
-
-enum MemKind { MEM_HOST = 0, MEM_DEVICE = 1 };
-
-MemKind mem_kind(const void *p, int *dev)
-{
-    hipPointerAttribute_t a;
-    memset(&a, 0, sizeof(a));
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void) hipGetLastError();  // unregistered pageable host memory
-        return MEM_HOST;
-    }
-    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
-        a.type == hipMemoryTypeUnified) {
-        if (dev) *dev = a.device;
-        return MEM_DEVICE;
-    }
-    return MEM_HOST;
-}
-
-bool ranges_overlap(const void *a, const void *b, size_t n)
-{
-    // byte-exact: the reference's OVERLAP_CHECK (src/reductions.c:27-30)
-    // adds a byte count to a typed pointer and over-detects by sizeof(T)
-    uintptr_t x = (uintptr_t) a, y = (uintptr_t) b;
-    return (x < y + n) && (y < x + n);
-}
-
-void fold_order(int me, int PE_start, int step, int PE_size, int *order)
-{
-    int k = 0;
-    order[k++] = me;
-    for (int i = 0, pe = PE_start; i < PE_size; i++, pe += step)
-        if (pe != me) order[k++] = pe;
-}
+using namespace osgpu::rt;
 
 // ------------------------------------------------------------- the paths
 
-struct Call {
-    const char *name;
-    int type, op;
-    void *target, *source;
-    int nreduce, PE_start, logPE_stride, PE_size;
-    long *pSync;
-    int me, step;
-    size_t nbytes;
-    PeOps ops;
+// one reduce-to-all call: the active set (Coll) plus the arrays
+struct Call : Coll {
+    int type = 0, op = 0;
+    void *target = nullptr, *source = nullptr;
+    int nreduce = 0;
+    size_t nbytes = 0;
 };
-
-void barrier(const Call &c)
-{
-    DBG("%s PE %d: barrier enter", c.name, c.me);
-    c.ops.barrier(c.PE_start, c.logPE_stride, c.PE_size, c.pSync);
-    DBG("%s PE %d: barrier exit", c.name, c.me);
-}
 
 bool p2p_sources(const Call &c, std::vector<const void *> &srcs)
 {
@@ -536,119 +191,6 @@ void run_rccl(const Call &c)
     }
 }
 
-// ---------------------------------------------------------------------
-// STAGED host path: H2D of my own source -> exchange ON THE GPUs (team
-// kernel over every PE's device staging buffers, IPC-mapped) -> D2H.
-// Pipelined over chunks with two slots and three streams:
-//   H2D(c+1) || team(c) || D2H(c-1).
-// The peers' data never crosses the host: PCIe carries N*s in and N*s out
-// per PE, xGMI carries the exchange.  Setup (once per active set) publishes
-// each PE's staging allocation through spare words of the symmetric pSync
-// (the reference's barrier only uses pSync[0], src/shmemc/barrier.c:64-97)
-// and reads the peers' with shmem_getmem; pSync is returned zeroed.
-// ---------------------------------------------------------------------
-
-constexpr int kPsyncBase = 16;  // pSync[16..28] used during setup only
-
-struct StageSet {
-    bool ok = false;
-    int device = -1;
-    size_t slot = 0;                 // bytes per slot (in0, in1, out0, out1)
-    char *local = nullptr;
-    std::vector<char *> peer;        // by active-set index
-    std::vector<void *> opened;      // IPC mappings to close
-    hipStream_t st_in = nullptr, st_c = nullptr, st_out = nullptr;
-    hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
-    char *in(int i, int s) const { return peer[i] + (size_t) s * slot; }
-    char *out(int i, int s) const { return peer[i] + (size_t) (2 + s) * slot; }
-};
-
-std::map<std::tuple<int, int, int, int, int>, StageSet> g_stage;  // (me, set, device)
-
-size_t stage_slot_bytes()
-{
-    const char *e = getenv("OSGPU_STAGE_BYTES");
-    size_t b = e ? strtoull(e, nullptr, 0) : 0;
-    b = b ? b : (size_t) 32 << 20;
-    return (b + 255) & ~(size_t) 255;
-}
-
-struct StageMsg {  // what a PE publishes in pSync[16..28]
-    long handle[OSGPU_IPC_HANDLE_BYTES / sizeof(long)];
-    long raw_ptr, pid, slot, status, pad[3];
-};
-static_assert(sizeof(StageMsg) <= (128 - kPsyncBase) * sizeof(long), "pSync room");
-
-StageSet *stage_setup(const Call &c)
-{
-    int dev = 0;
-    HIPCHK(c.name, hipGetDevice(&dev));
-    auto key = std::make_tuple(c.me, c.PE_start, c.step, c.PE_size, dev);
-    std::unique_lock<std::mutex> lk(g_mu);
-    auto it = g_stage.find(key);
-    if (it != g_stage.end()) return it->second.ok ? &it->second : nullptr;
-    StageSet &S = g_stage[key];  // std::map: the reference stays valid
-    lk.unlock();
-    S.device = dev;
-    S.slot = stage_slot_bytes();
-    HIPCHK(c.name, hipMalloc((void **) &S.local, 4 * S.slot));
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_in, hipStreamNonBlocking));
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_c, hipStreamNonBlocking));
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_out, hipStreamNonBlocking));
-    for (int s = 0; s < 2; s++) {
-        HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_in[s], hipEventDisableTiming));
-        HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_out[s], hipEventDisableTiming));
-    }
-    StageMsg *mine = reinterpret_cast<StageMsg *>(c.pSync + kPsyncBase);
-    memset(mine, 0, sizeof(*mine));
-    hipIpcMemHandle_t h;
-    if (hipIpcGetMemHandle(&h, S.local) == hipSuccess) memcpy(mine->handle, &h, sizeof(h));
-    else (void) hipGetLastError();
-    mine->raw_ptr = (long) (uintptr_t) S.local;
-    mine->pid = (long) getpid();
-    mine->slot = (long) S.slot;
-    barrier(c);
-    bool ok = true;
-    S.peer.assign(c.PE_size, nullptr);
-    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
-        if (pe == c.me) {
-            S.peer[i] = S.local;
-            continue;
-        }
-        StageMsg m;
-        c.ops.getmem(&m, mine, sizeof(m), pe);
-        if ((size_t) m.slot != S.slot) {
-            ok = false;
-        } else if (m.pid == (long) getpid()) {
-            S.peer[i] = (char *) (uintptr_t) m.raw_ptr;   // same process (threads as PEs)
-        } else {
-            hipIpcMemHandle_t ph;
-            memcpy(&ph, m.handle, sizeof(ph));
-            void *p = nullptr;
-            if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
-                S.peer[i] = (char *) p;
-                S.opened.push_back(p);
-            } else {
-                (void) hipGetLastError();
-                ok = false;
-            }
-        }
-    }
-    mine->status = ok ? 1 : 2;
-    barrier(c);
-    bool all_ok = ok;
-    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
-        if (pe == c.me) continue;
-        long st = 0;
-        c.ops.getmem(&st, &mine->status, sizeof(long), pe);
-        all_ok = all_ok && st == 1;
-    }
-    barrier(c);
-    memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
-    S.ok = all_ok;
-    return S.ok ? &S : nullptr;
-}
-
 void run_staged(const Call &c, StageSet &S)
 {
     const size_t s = type_size(c.type);
@@ -785,26 +327,13 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
             int PE_start, int logPE_stride, int PE_size, void *pWrk, long *pSync)
 {
     (void) pWrk;  // the combine needs no bounce buffer: peers are read directly
-    if (PE_size < 1 || PE_start < 0 || logPE_stride < 0 || logPE_stride > 30)
-        fatal(name, "invalid active set (PE_start=%d logPE_stride=%d PE_size=%d)", PE_start,
-              logPE_stride, PE_size);
     Call c;
-    c.name = name;
+    static_cast<Coll &>(c) = make_coll(name, PE_start, logPE_stride, PE_size, pSync);
     c.type = type;
     c.op = op;
     c.target = target;
     c.source = source;
     c.nreduce = nreduce;
-    c.PE_start = PE_start;
-    c.logPE_stride = logPE_stride;
-    c.PE_size = PE_size;
-    c.pSync = pSync;
-    c.step = 1 << logPE_stride;
-    c.ops = pe_ops();
-    if (!c.ops.my_pe || !c.ops.barrier)
-        fatal(name, "no OpenSHMEM runtime: shmem_my_pe/shmem_barrier not found "
-                    "(link the OpenSHMEM library or call osgpu_set_pe_ops)");
-    c.me = c.ops.my_pe();
     if (nreduce <= 0) {  // nothing to combine; the collective still syncs
         barrier(c);
         barrier(c);
@@ -908,270 +437,3 @@ OSGPU_DEFINE_MINMAX(longlong, long long, OSGPU_T_LONGLONG)
 OSGPU_DEFINE_MINMAX(float, float, OSGPU_T_FLOAT)
 OSGPU_DEFINE_MINMAX(double, double, OSGPU_T_DOUBLE)
 OSGPU_DEFINE_MINMAX(longdouble, long double, OSGPU_T_LONGDOUBLE)
-
-// ======================================================================
-// Part 2: control surface
-// ======================================================================
-
-extern "C" {
-
-int osgpu_set_pe_ops(const osgpu_pe_ops *ops)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!ops) {
-        g_ops = PeOps();
-        g_ops_set = false;
-        return OSGPU_OK;
-    }
-    if (!ops->my_pe || !ops->barrier) {
-        set_err("osgpu_set_pe_ops: my_pe and barrier are required");
-        return OSGPU_EINVAL;
-    }
-    g_ops.my_pe = ops->my_pe;
-    g_ops.n_pes = ops->n_pes;
-    g_ops.barrier = ops->barrier;
-    g_ops.getmem = ops->getmem;
-    g_ops_set = true;
-    return OSGPU_OK;
-}
-
-int osgpu_heap_register_segment(int pe, int seg, void *base, size_t bytes)
-{
-    if (pe < 0 || seg < 0 || seg > 255 || !base || !bytes) {
-        set_err("osgpu_heap_register_segment: bad arguments");
-        return OSGPU_EINVAL;
-    }
-    std::lock_guard<std::mutex> lk(g_mu);
-    if ((size_t) pe >= g_heap.size()) g_heap.resize(pe + 1);
-    if ((size_t) seg >= g_heap[pe].size()) g_heap[pe].resize(seg + 1);
-    g_heap[pe][seg].base = (char *) base;
-    g_heap[pe][seg].bytes = bytes;
-    return OSGPU_OK;
-}
-
-int osgpu_heap_register(int pe, void *base, size_t bytes)
-{
-    return osgpu_heap_register_segment(pe, 0, base, bytes);
-}
-
-int osgpu_heap_unregister(int pe)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (pe < 0 || (size_t) pe >= g_heap.size()) return OSGPU_EINVAL;
-    g_heap[pe].clear();
-    return OSGPU_OK;
-}
-
-void *osgpu_heap_translate(const void *addr, int from_pe, int to_pe)
-{
-    int seg = -1;
-    size_t off = 0;
-    char *p = nullptr;
-    if (!heap_locate(from_pe, addr, 1, &seg, &off) || !heap_peer(to_pe, seg, off, 1, &p))
-        return nullptr;
-    return p;
-}
-
-int osgpu_ipc_get_handle(void *dev_base, void *handle_out)
-{
-    static_assert(sizeof(hipIpcMemHandle_t) <= OSGPU_IPC_HANDLE_BYTES, "ipc handle size");
-    hipIpcMemHandle_t h;
-    hipError_t e = hipIpcGetMemHandle(&h, dev_base);
-    if (e != hipSuccess) {
-        set_err("hipIpcGetMemHandle: %s", hipGetErrorString(e));
-        return OSGPU_EHIP;
-    }
-    memset(handle_out, 0, OSGPU_IPC_HANDLE_BYTES);
-    memcpy(handle_out, &h, sizeof(h));
-    return OSGPU_OK;
-}
-
-void *osgpu_ipc_open(const void *handle)
-{
-    hipIpcMemHandle_t h;
-    memcpy(&h, handle, sizeof(h));
-    void *p = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) {
-        set_err("hipIpcOpenMemHandle: %s", hipGetErrorString(e));
-        return nullptr;
-    }
-    return p;
-}
-
-int osgpu_ipc_close(void *mapped)
-{
-    hipError_t e = hipIpcCloseMemHandle(mapped);
-    if (e != hipSuccess) {
-        set_err("hipIpcCloseMemHandle: %s", hipGetErrorString(e));
-        return OSGPU_EHIP;
-    }
-    return OSGPU_OK;
-}
-
-int osgpu_rccl_unique_id(void *uid_out)
-{
-    static_assert(sizeof(ncclUniqueId) == OSGPU_RCCL_UID_BYTES, "uid size");
-    ncclUniqueId id;
-    ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) {
-        set_err("ncclGetUniqueId: %s", ncclGetErrorString(r));
-        return OSGPU_ERCCL;
-    }
-    memcpy(uid_out, &id, sizeof(id));
-    return OSGPU_OK;
-}
-
-int osgpu_rccl_init(int npes, int me, const void *uid)
-{
-    if (g_rccl.world) return OSGPU_OK;
-    ncclUniqueId id;
-    memcpy(&id, uid, sizeof(id));
-    ncclComm_t comm;
-    ncclResult_t r = ncclCommInitRank(&comm, npes, id, me);
-    if (r != ncclSuccess) {
-        set_err("ncclCommInitRank: %s", ncclGetErrorString(r));
-        return OSGPU_ERCCL;
-    }
-    g_rccl.world = comm;
-    g_rccl.npes = npes;
-    g_rccl.me = me;
-    return OSGPU_OK;
-}
-
-int osgpu_rccl_finalize(void)
-{
-    if (!g_rccl.world) return OSGPU_OK;
-    ncclResult_t r = ncclCommDestroy(g_rccl.world);
-    g_rccl = Rccl();
-    return r == ncclSuccess ? OSGPU_OK : OSGPU_ERCCL;
-}
-
-int osgpu_finalize(void)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &kv : g_stage) {
-        StageSet &S = kv.second;
-        for (void *p : S.opened) (void) hipIpcCloseMemHandle(p);
-        if (S.local) (void) hipFree(S.local);
-        for (int s = 0; s < 2; s++) {
-            if (S.ev_in[s]) (void) hipEventDestroy(S.ev_in[s]);
-            if (S.ev_out[s]) (void) hipEventDestroy(S.ev_out[s]);
-        }
-        if (S.st_in) (void) hipStreamDestroy(S.st_in);
-        if (S.st_c) (void) hipStreamDestroy(S.st_c);
-        if (S.st_out) (void) hipStreamDestroy(S.st_out);
-    }
-    g_stage.clear();
-    for (auto &kv : g_pectx) {
-        PeCtx *x = kv.second;
-        if (x->dscratch) (void) hipFree(x->dscratch);
-        if (x->hstage) (void) hipHostFree(x->hstage);
-        if (x->stream) (void) hipStreamDestroy(x->stream);
-        delete x;
-    }
-    g_pectx.clear();
-    (void) hipGetLastError();
-    return OSGPU_OK;
-}
-
-int osgpu_host_register(void *base, size_t bytes)
-{
-    hipError_t e = hipHostRegister(base, bytes, hipHostRegisterDefault);
-    if (e != hipSuccess) {
-        set_err("hipHostRegister: %s", hipGetErrorString(e));
-        return OSGPU_EHIP;
-    }
-    return OSGPU_OK;
-}
-
-int osgpu_host_unregister(void *base)
-{
-    hipError_t e = hipHostUnregister(base);
-    if (e != hipSuccess) {
-        set_err("hipHostUnregister: %s", hipGetErrorString(e));
-        return OSGPU_EHIP;
-    }
-    return OSGPU_OK;
-}
-
-int osgpu_set_path(int path)
-{
-    if (path < OSGPU_PATH_AUTO || path > OSGPU_PATH_PULL) return OSGPU_EINVAL;
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_path = path;
-    return OSGPU_OK;
-}
-
-int osgpu_set_stream(void *hip_stream)
-{
-    t_ctx.stream = (hipStream_t) hip_stream;
-    t_ctx.user_stream = hip_stream != nullptr;
-    if (!hip_stream) t_ctx.device = -1;
-    return OSGPU_OK;
-}
-
-void *osgpu_get_stream(void)
-{
-    return (void *) thread_stream("osgpu_get_stream");
-}
-
-int osgpu_combine(int type, int op, void *target, const void *const *srcs, int nsrc,
-                  size_t nelems, void *hip_stream)
-{
-    if (!has_op(type, op) || nsrc < 1 || !target || !srcs) {
-        set_err("osgpu_combine: bad arguments");
-        return OSGPU_EINVAL;
-    }
-    hipStream_t st = hip_stream ? (hipStream_t) hip_stream : thread_stream("osgpu_combine");
-    hipError_t e = osgpu::launch_combine(type, op, target, srcs, nsrc, nelems, st);
-    if (e == hipErrorNotSupported) {
-        set_err("osgpu_combine: type %d op %d not supported on the GPU", type, op);
-        return OSGPU_ENOTSUP;
-    }
-    if (e != hipSuccess) {
-        set_err("osgpu_combine: %s", hipGetErrorString(e));
-        return OSGPU_EHIP;
-    }
-    return OSGPU_OK;
-}
-
-int osgpu_has_op(int type, int op) { return has_op(type, op) ? 1 : 0; }
-
-size_t osgpu_type_size(int type) { return type_size(type); }
-
-int osgpu_fold_order(int me, int PE_start, int logPE_stride, int PE_size, int *order_out)
-{
-    if (PE_size < 1 || logPE_stride < 0 || logPE_stride > 30 || !order_out)
-        return OSGPU_EINVAL;
-    const int step = 1 << logPE_stride;
-    bool member = false;
-    for (int i = 0; i < PE_size; i++) member |= (PE_start + i * step == me);
-    if (!member) return OSGPU_EINVAL;
-    fold_order(me, PE_start, step, PE_size, order_out);
-    return OSGPU_OK;
-}
-
-int osgpu_shard_range(long long nreduce, int PE_size, int idx, int elem_bytes, long long *lo,
-                      long long *hi)
-{
-    if (nreduce < 0 || PE_size < 1 || idx < 0 || idx >= PE_size || elem_bytes < 1 ||
-        elem_bytes > 16 || !lo || !hi)
-        return OSGPU_EINVAL;
-    // shard boundaries on 16-byte vector granules so every shard stays on
-    // the vector path; the last shard takes the ragged remainder
-    const long long g = elem_bytes >= 16 ? 1 : 16 / elem_bytes;
-    const long long granules = nreduce / g;
-    const long long base = granules / PE_size, rem = granules % PE_size;
-    const long long start = idx * base + (idx < rem ? idx : rem);
-    const long long cnt = base + (idx < rem ? 1 : 0);
-    *lo = start * g;
-    *hi = (idx == PE_size - 1) ? nreduce : (start + cnt) * g;
-    return OSGPU_OK;
-}
-
-const char *osgpu_last_error(void) { return g_err; }
-
-const char *osgpu_version(void) { return "osgpu_reduce 0.1 (gfx950)"; }
-
-}  // extern "C"

@@ -42,6 +42,9 @@ def has_op(t: str, op: str) -> bool:
 
 ENTRY_POINTS = [f"shmem_{t}_{o}_to_all" for o in OPS for t in TYPES if has_op(t, o)]
 assert len(ENTRY_POINTS) == 44
+# data-movement collectives on the same machinery (include/osgpu_reduce.h Part 1b)
+COLL_KINDS = ["broadcast", "collect", "fcollect", "alltoall"]
+COLL_ENTRY_POINTS = [f"shmem_{k}{b}" for k in COLL_KINDS for b in (32, 64)]
 
 
 class PeOps(ctypes.Structure):
@@ -92,6 +95,15 @@ def load() -> ctypes.CDLL:
             f = getattr(L, pfx + name)
             f.argtypes = [vp, vp, i, i, i, i, vp, vp]
             f.restype = None
+    sz_t, lp = ctypes.c_size_t, ctypes.c_void_p
+    for name in COLL_ENTRY_POINTS:
+        for pfx in ("", "p"):
+            f = getattr(L, pfx + name)
+            if "broadcast" in name:
+                f.argtypes = [vp, vp, sz_t, i, i, i, i, lp]
+            else:
+                f.argtypes = [vp, vp, sz_t, i, i, i, lp]
+            f.restype = None
     L.osgpu_set_pe_ops.argtypes = [vp]
     L.osgpu_heap_register.argtypes = [i, vp, sz]
     L.osgpu_heap_register_segment.argtypes = [i, i, vp, sz]
@@ -139,6 +151,11 @@ def combine(t: str, op: str, target: int, srcs, n: int, stream: int | None = Non
                            f"{L.osgpu_last_error().decode()}")
 
 
+def coll(kind: str, bits: int):
+    """The ctypes function shmem_<kind><bits> (broadcast/collect/fcollect/alltoall)."""
+    return getattr(load(), f"shmem_{kind}{bits}")
+
+
 def fold_order(me, PE_start, logPE_stride, PE_size):
     out = (ctypes.c_int * PE_size)()
     rc = load().osgpu_fold_order(me, PE_start, logPE_stride, PE_size, out)
@@ -164,6 +181,6 @@ def header_symbols(path: str = HEADER):
     names = set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(osgpu_\w+)\s*\(",
                            src, re.M))
     for pfx in ("shmem_", "pshmem_"):
-        for e in ENTRY_POINTS:
+        for e in ENTRY_POINTS + COLL_ENTRY_POINTS:
             names.add(pfx + e[len("shmem_"):])
     return sorted(names)

@@ -71,6 +71,14 @@ class Team:
             self.base = self.buf.data_ptr()
             for pe in range(npes):
                 assert self.lib.osgpu_heap_register(pe, self.base + pe * self.H, self.H) == 0
+            # pSync is host memory in every OpenSHMEM program: a small host
+            # symmetric heap per PE holds it (getmem-able, like the UCX heap)
+            self.pbuf = np.zeros(npes * 4096 + 256, dtype=np.uint8)
+            a = self.pbuf.ctypes.data
+            self.poff = (-a) % 256
+            self.pbase = a + self.poff
+            for pe in range(npes):
+                assert self.pet.pet_register_host_heap(pe, self.pbase + pe * 4096, 4096) == 0
         else:
             self.hbuf = np.zeros(npes * self.H + 256, dtype=np.uint8)
             a = self.hbuf.ctypes.data
@@ -118,24 +126,32 @@ class Team:
         if members is None:
             members = [PE_start + i * step for i in range(PE_size)]
         fn = self.osgpu.to_all(t, op)
-        psync = (ctypes.c_long * 128)()
         pwrk = (ctypes.c_byte * 4096)()
-        errs = []
+        self._on_members(members, lambda pe: fn(
+            self.ptr(pe, target_off), self.ptr(pe, source_off), nreduce, PE_start,
+            logPE_stride, PE_size, ctypes.addressof(pwrk), self.psync_ptr(pe)))
 
-        def psync_ptr(pe):
-            # host heaps: symmetric pSync inside the heap (the staged host
-            # path reads peers' pSync words with getmem); device heaps: a host
-            # array (pSync is host memory in every OpenSHMEM program)
-            if self.device:
-                return ctypes.addressof(psync)
-            return self.ptr(pe, self.psync_off)
+    def psync_ptr(self, pe: int) -> int:
+        """PE pe's symmetric pSync (host memory, getmem-able): inside the
+        host heap, or in the small host heap of a device team."""
+        if self.device:
+            return self.pbase + pe * 4096
+        return self.ptr(pe, self.psync_off)
+
+    def psync_bytes(self, pe: int) -> np.ndarray:
+        if self.device:
+            return self.pbuf[self.poff + pe * 4096:][:1024]
+        return self.hbuf[self.hoff + pe * self.H + self.psync_off:][:1024]
+
+    def _on_members(self, members, call):
+        """Run call(pe) on one thread per member PE (a blocking collective),
+        then check every member's pSync is back at SHMEM_SYNC_VALUE."""
+        errs = []
 
         def body(pe):
             try:
                 self.pet.pet_set_me(pe)
-                fn(self.ptr(pe, target_off), self.ptr(pe, source_off), nreduce,
-                   PE_start, logPE_stride, PE_size, ctypes.addressof(pwrk),
-                   psync_ptr(pe))
+                call(pe)
             except Exception as e:  # pragma: no cover
                 errs.append(e)
 
@@ -146,11 +162,27 @@ class Team:
             th.join()
         if errs:
             raise errs[0]
-        assert all(v == 0 for v in psync), "pSync must be left at SHMEM_SYNC_VALUE"
-        if not self.device:
-            for pe in members:
-                ps = self.hbuf[self.hoff + pe * self.H + self.psync_off:][:1024]
-                assert not ps.any(), "pSync must be left at SHMEM_SYNC_VALUE"
+        for pe in members:
+            assert not self.psync_bytes(pe).any(), "pSync must be left at SHMEM_SYNC_VALUE"
+
+    def run_coll(self, kind: str, bits: int, target_off: int, source_off: int, nelems,
+                 PE_root: int = 0, PE_start: int = 0, logPE_stride: int = 0,
+                 PE_size: int | None = None):
+        """Every member calls shmem_<kind><bits> on its own thread.  nelems:
+        one count, or {pe: count} (collect's contributions differ per PE)."""
+        if PE_size is None:
+            PE_size = self.npes
+        step = 1 << logPE_stride
+        members = [PE_start + i * step for i in range(PE_size)]
+        fn = self.osgpu.coll(kind, bits)
+        cnt = (lambda pe: nelems[pe]) if isinstance(nelems, dict) else (lambda pe: nelems)
+        if kind == "broadcast":
+            call = lambda pe: fn(self.ptr(pe, target_off), self.ptr(pe, source_off), cnt(pe),
+                                 PE_root, PE_start, logPE_stride, PE_size, self.psync_ptr(pe))
+        else:
+            call = lambda pe: fn(self.ptr(pe, target_off), self.ptr(pe, source_off), cnt(pe),
+                                 PE_start, logPE_stride, PE_size, self.psync_ptr(pe))
+        self._on_members(members, call)
 
 
 X87_PATH = os.path.join(HERE, "libx87check.so")
