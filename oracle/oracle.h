@@ -74,6 +74,14 @@ double oracle_cpu_baseline(int type, int op, int npes,
                            const void *const *sources, void *const *targets,
                            int nreduce, int reps, int pin_cores);
 
+/*
+ * CPU baseline of the data-movement collectives (oracle_coll.c): kind 0
+ * broadcast, 1 collect, 2 fcollect, 3 alltoall, in the reference's loop
+ * shape; nb bytes per PE contribution; median seconds per call.
+ */
+double oracle_coll_baseline(int kind, int npes, char *const *src, char *const *tgt, size_t nb,
+                            int root, int reps, int pin_cores);
+
 #ifdef __cplusplus
 }
 #endif

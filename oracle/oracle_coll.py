@@ -84,3 +84,28 @@ def alltoall(sources: dict, targets: dict, nbytes: int, PE_start: int,
         for i, pe in enumerate(pes):
             out[me][i * nbytes:(i + 1) * nbytes] = sources[pe][b * nbytes:(b + 1) * nbytes]
     return out
+
+
+COLL_KINDS = ["broadcast", "collect", "fcollect", "alltoall"]
+
+
+def cpu_baseline(kind: str, npes: int, nb: int, root: int = 0, reps: int = 5,
+                 pin: bool = True) -> float:
+    """Median seconds per call of the reference loop shape (oracle_coll.c),
+    one pthread per PE, nb bytes per PE contribution."""
+    import ctypes
+    import oracle as O
+    L = O.lib()
+    f = L.oracle_coll_baseline
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    sb = npes * nb if kind == "alltoall" else nb
+    srcs = [np.random.default_rng(pe).integers(0, 256, sb, dtype=np.uint8) for pe in range(npes)]
+    tgts = [np.empty(npes * nb, np.uint8) for _ in range(npes)]
+    sp = (ctypes.c_void_p * npes)(*[s.ctypes.data for s in srcs])
+    tp = (ctypes.c_void_p * npes)(*[t.ctypes.data for t in tgts])
+    sec = f(COLL_KINDS.index(kind), npes, sp, tp, nb, root, reps, 1 if pin else 0)
+    if sec < 0:
+        raise ValueError("bad baseline arguments")
+    return sec

@@ -13,6 +13,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -376,11 +377,25 @@ size_t stage_slot_bytes()
     return (b + 255) & ~(size_t) 255;
 }
 
-struct StageMsg {  // what a PE publishes in pSync[16..28]
+struct StageMsg {  // what a PE publishes in pSync[16..30]
     long handle[OSGPU_IPC_HANDLE_BYTES / sizeof(long)];
-    long raw_ptr, pid, slot, status, pad[3];
+    long raw_ptr, pid, slot, status, pci, pad[2];
 };
-static_assert(sizeof(StageMsg) <= (128 - kPsyncBase) * sizeof(long), "pSync room");
+// the smallest pSync a caller hands us: SHMEM_BCAST/COLLECT/ALLTOALL_SYNC_SIZE
+static_assert(sizeof(StageMsg) <= (64 - kPsyncBase) * sizeof(long), "pSync room");
+
+// PCI location of a device: PEs with equal keys share one GPU and its link
+long pci_key(int dev)
+{
+    int dom = 0, bus = 0, d = 0;
+    if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&d, hipDeviceAttributePciDeviceId, dev) != hipSuccess) {
+        (void) hipGetLastError();
+        return -1 - dev;
+    }
+    return ((long) dom << 16 | (long) bus << 8 | d) + 1;
+}
 
 StageSet *stage_setup(const Coll &c)
 {
@@ -410,9 +425,11 @@ StageSet *stage_setup(const Coll &c)
     mine->raw_ptr = (long) (uintptr_t) S.local;
     mine->pid = (long) getpid();
     mine->slot = (long) S.slot;
+    mine->pci = pci_key(dev);
     barrier(c);
     bool ok = true;
     S.peer.assign(c.PE_size, nullptr);
+    std::vector<long> pcis(1, mine->pci);
     for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
         if (pe == c.me) {
             S.peer[i] = S.local;
@@ -420,6 +437,7 @@ StageSet *stage_setup(const Coll &c)
         }
         StageMsg m;
         c.ops.getmem(&m, mine, sizeof(m), pe);
+        if (std::find(pcis.begin(), pcis.end(), m.pci) == pcis.end()) pcis.push_back(m.pci);
         if ((size_t) m.slot != S.slot) {
             ok = false;
         } else if (m.pid == (long) getpid()) {
@@ -448,6 +466,7 @@ StageSet *stage_setup(const Coll &c)
     }
     barrier(c);
     memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
+    S.ndev = (int) pcis.size();
     S.ok = all_ok;
     return S.ok ? &S : nullptr;
 }
@@ -680,6 +699,27 @@ int osgpu_combine(int type, int op, void *target, const void *const *srcs, int n
     if (e != hipSuccess) {
         set_err("osgpu_combine: %s", hipGetErrorString(e));
         return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
+int osgpu_copy(void *const *dsts, const void *const *srcs, const size_t *bytes, int n,
+               void *hip_stream)
+{
+    if (n < 0 || (n > 0 && (!dsts || !srcs || !bytes))) {
+        set_err("osgpu_copy: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    hipStream_t st = hip_stream ? (hipStream_t) hip_stream : thread_stream("osgpu_copy");
+    for (int i = 0; i < n; i += osgpu::kMaxCopySegs) {
+        osgpu::CopySeg seg[osgpu::kMaxCopySegs];
+        const int m = n - i < osgpu::kMaxCopySegs ? n - i : osgpu::kMaxCopySegs;
+        for (int j = 0; j < m; j++) seg[j] = {srcs[i + j], dsts[i + j], bytes[i + j]};
+        hipError_t e = osgpu::launch_copy(seg, m, st);
+        if (e != hipSuccess) {
+            set_err("osgpu_copy: %s", hipGetErrorString(e));
+            return OSGPU_EHIP;
+        }
     }
     return OSGPU_OK;
 }

@@ -127,6 +127,7 @@ void barrier(const Coll &c);
 struct StageSet {
     bool ok = false;
     int device = -1;
+    int ndev = 0;                    // distinct GPUs (PCI locations) among the members
     size_t slot = 0;                 // bytes per slot (in0, in1, out0, out1)
     char *local = nullptr;
     std::vector<char *> peer;        // by active-set index

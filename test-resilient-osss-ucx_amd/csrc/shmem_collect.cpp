@@ -25,10 +25,13 @@
 //           (sources ready / every reader done);
 //   RCCL    device-resident without registered heaps, one process per GPU,
 //           whole job: ncclBroadcast / ncclAllGather (broadcast, fcollect);
-//   STAGED  host arguments: H2D my source -> copy kernel over every PE's
-//           IPC-mapped device staging -> D2H of my target, chunked;
-//   GETMEM  host arguments when staging cannot be mapped: the reference's
-//           own linear algorithm over the runtime's shmem_getmem.
+//   STAGED  host arguments, every member on a GPU of its own: H2D my source
+//           -> copy kernel over every PE's IPC-mapped device staging -> D2H
+//           of my target, chunked (each PE's PCIe link carries its bytes);
+//   GETMEM  host arguments when members share a GPU (and so its PCIe link)
+//           or staging cannot be mapped: the reference's own linear
+//           algorithm over the runtime's shmem_getmem -- pure byte movement,
+//           which the runtime's memcpy does at memory speed.
 //
 // collect needs every PE's nelems before any byte moves: each PE publishes
 // it in a spare pSync word (the reference's barrier uses pSync[0] only,
@@ -366,11 +369,17 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
             fatal(name, "no GPU visible: the collectives run on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
+        // STAGED moves 1 + P (in + out) bytes per target byte over each
+        // PE's PCIe link; that beats the runtime's memcpy only when every
+        // member has a GPU (and a link) of its own -- PEs sharing a GPU
+        // share its link (tools/coll_bench.py).
+        // OSGPU_HOST_PATH=staged|getmem overrides.
         const char *hp = getenv("OSGPU_HOST_PATH");
-        const bool getmem_only = hp && !strcmp(hp, "getmem");
+        const bool force_getmem = hp && !strcmp(hp, "getmem");
+        const bool force_staged = hp && !strcmp(hp, "staged");
         if (!counts_done) barrier(c);  // sources ready (staging setup runs after it)
-        StageSet *S = getmem_only ? nullptr : stage_setup(c);
-        if (S) run_staged(c, *S);
+        StageSet *S = force_getmem ? nullptr : stage_setup(c);
+        if (S && (force_staged || S->ndev == c.PE_size || c.PE_size == 1)) run_staged(c, *S);
         else run_getmem(c);
         barrier(c);
         if (kind == K_COLLECT) c.pSync[kCountWord] = 0;

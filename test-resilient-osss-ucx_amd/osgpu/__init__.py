@@ -120,6 +120,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_set_stream.argtypes = [vp]
     L.osgpu_get_stream.restype = vp
     L.osgpu_combine.argtypes = [i, i, vp, vp, i, sz, vp]
+    L.osgpu_copy.argtypes = [vp, vp, vp, i, vp]
     L.osgpu_has_op.argtypes = [i, i]
     L.osgpu_type_size.argtypes = [i]
     L.osgpu_type_size.restype = sz
@@ -149,6 +150,16 @@ def combine(t: str, op: str, target: int, srcs, n: int, stream: int | None = Non
     if rc != 0:
         raise RuntimeError(f"osgpu_combine({t},{op}) = {rc}: "
                            f"{L.osgpu_last_error().decode()}")
+
+
+def copy(dsts, srcs, nbytes, stream: int | None = None):
+    """Enqueue the collectives' copy kernel: dsts[i][:nbytes[i]] = srcs[i][...]."""
+    L = load()
+    n = len(dsts)
+    rc = L.osgpu_copy((ctypes.c_void_p * n)(*dsts), (ctypes.c_void_p * n)(*srcs),
+                      (ctypes.c_size_t * n)(*nbytes), n, stream)
+    if rc != 0:
+        raise RuntimeError(f"osgpu_copy = {rc}: {L.osgpu_last_error().decode()}")
 
 
 def coll(kind: str, bits: int):

@@ -119,6 +119,9 @@ static pe_ops_t g_table = {pet_my_pe, pet_n_pes, pet_barrier, pet_getmem};
    shmem_<T>_<op>_to_all) `reps` times; PE 0 times each collective call from
    a common start (pthread barrier) to its own return, after one warm-up. */
 typedef void (*to_all_fn)(void *, void *, int, int, int, int, void *, long *);
+/* shmem_collect/fcollect/alltoall<bits> and shmem_broadcast<bits> */
+typedef void (*coll_fn)(void *, const void *, size_t, int, int, int, long *);
+typedef void (*bcast_fn)(void *, const void *, size_t, int, int, int, int, long *);
 
 typedef struct {
     to_all_fn fn;
@@ -126,6 +129,9 @@ typedef struct {
     void **tgt, **src, **psync;
     pthread_barrier_t *bar;
     double *times;
+    int kind;        /* 0 to_all, 1 collect-like, 2 broadcast */
+    size_t nelems;   /* kinds 1, 2 */
+    int root;        /* kind 2 */
 } timing_arg;
 
 #include <time.h>
@@ -146,7 +152,14 @@ static void *timing_body(void *p)
     for (int r = 0; r <= a->reps; r++) {
         pthread_barrier_wait(a->bar);
         double t0 = now_s();
-        a->fn(a->tgt[a->me], a->src[a->me], a->n, 0, 0, a->npes, wrk, psync);
+        if (a->kind == 0)
+            a->fn(a->tgt[a->me], a->src[a->me], a->n, 0, 0, a->npes, wrk, psync);
+        else if (a->kind == 1)
+            ((coll_fn) (void *) a->fn)(a->tgt[a->me], a->src[a->me], a->nelems, 0, 0, a->npes,
+                                       psync);
+        else
+            ((bcast_fn) (void *) a->fn)(a->tgt[a->me], a->src[a->me], a->nelems, a->root, 0, 0,
+                                        a->npes, psync);
         pthread_barrier_wait(a->bar);
         if (a->me == 0) a->times[r] = now_s() - t0;
     }
@@ -159,8 +172,8 @@ static int cmpd(const void *x, const void *y)
     return a < b ? -1 : a > b;
 }
 
-double pet_time_to_all(void *fn, int npes, void **tgt, void **src, void **psync, int n,
-                       int reps)
+static double time_calls(void *fn, int kind, int npes, void **tgt, void **src, void **psync,
+                         int n, size_t nelems, int root, int reps)
 {
     if (npes < 1 || npes > MAXPE || reps < 1) return -1.0;
     pthread_barrier_t bar;
@@ -169,7 +182,8 @@ double pet_time_to_all(void *fn, int npes, void **tgt, void **src, void **psync,
     pthread_t th[MAXPE];
     timing_arg args[MAXPE];
     for (int i = 0; i < npes; i++) {
-        args[i] = (timing_arg){(to_all_fn) fn, npes, n, reps, i, tgt, src, psync, &bar, times};
+        args[i] = (timing_arg){(to_all_fn) fn, npes, n, reps, i, tgt, src, psync, &bar, times,
+                               kind, nelems, root};
         pthread_create(&th[i], NULL, timing_body, &args[i]);
     }
     for (int i = 0; i < npes; i++) pthread_join(th[i], NULL);
@@ -178,6 +192,20 @@ double pet_time_to_all(void *fn, int npes, void **tgt, void **src, void **psync,
     double med = times[1 + reps / 2];
     free(times);
     return med;
+}
+
+double pet_time_to_all(void *fn, int npes, void **tgt, void **src, void **psync, int n,
+                       int reps)
+{
+    return time_calls(fn, 0, npes, tgt, src, psync, n, 0, 0, reps);
+}
+
+/* fn = shmem_{collect,fcollect,alltoall}<bits> (root < 0) or
+   shmem_broadcast<bits> (root = PE_root); whole team, median seconds */
+double pet_time_coll(void *fn, int npes, void **tgt, void **src, void **psync, size_t nelems,
+                     int root, int reps)
+{
+    return time_calls(fn, root < 0 ? 1 : 2, npes, tgt, src, psync, 0, nelems, root, reps);
 }
 
 const void *pet_ops(void) { return &g_table; }

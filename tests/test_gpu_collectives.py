@@ -9,6 +9,7 @@ device staging -> D2H), also with tiny staging slots to force many chunks,
 and the GETMEM path.  Every byte of every member's target region is compared,
 including the margins the collective must not write; pSync must come back at
 SHMEM_SYNC_VALUE (checked by Team)."""
+import contextlib
 import os
 
 import numpy as np
@@ -22,6 +23,22 @@ pytestmark = pytest.mark.gpu
 
 SRC_OFF = 0
 MARGIN = 256
+MODES = ["device", "host", "staged"]  # host = auto (GETMEM when PEs share a GPU)
+
+
+@contextlib.contextmanager
+def host_path(mode):
+    """OSGPU_HOST_PATH for the duration of a case (read on every call)."""
+    old = os.environ.get("OSGPU_HOST_PATH")
+    if mode in ("staged", "getmem"):
+        os.environ["OSGPU_HOST_PATH"] = mode
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("OSGPU_HOST_PATH", None)
+        else:
+            os.environ["OSGPU_HOST_PATH"] = old
 
 
 def _layout(P, max_src_bytes):
@@ -115,22 +132,26 @@ def _run_case(device, kind, bits, setdef, nelems, root=0, seed=1, same_buffer=Fa
     return tm
 
 
-@pytest.mark.parametrize("device", [True, False], ids=["device", "host"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("kind", ["broadcast", "collect", "fcollect", "alltoall"])
 @pytest.mark.parametrize("bits", [32, 64])
 @pytest.mark.parametrize("setdef", SETS, ids=lambda s: "P%d_s%d_l%d_n%d" % s)
-def test_collective_matches_oracle(device, kind, bits, setdef):
-    for nelems in (1, 7, 1000, 4099):
-        root = (nelems % setdef[3]) if kind == "broadcast" else 0
-        _run_case(device, kind, bits, setdef, nelems, root=root, seed=nelems + bits)
+def test_collective_matches_oracle(mode, kind, bits, setdef):
+    with host_path(mode):
+        for nelems in (1, 7, 1000, 4099):
+            root = (nelems % setdef[3]) if kind == "broadcast" else 0
+            _run_case(mode != "device", kind, bits, setdef, nelems, root=root,
+                      seed=nelems + bits)
 
 
-@pytest.mark.parametrize("device", [True, False], ids=["device", "host"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("kind", ["broadcast", "collect", "fcollect", "alltoall"])
-def test_collective_source_is_target(device, kind):
+def test_collective_source_is_target(mode, kind):
     """target == source (same symmetric object): peers must read pre-call
     bytes (scratch / temporary target)."""
-    _run_case(device, kind, 64, (3, 0, 0, 3), 1001, root=1, seed=5, same_buffer=True)
+    with host_path(mode):
+        _run_case(mode != "device", kind, 64, (3, 0, 0, 3), 1001, root=1, seed=5,
+                  same_buffer=True)
 
 
 @pytest.mark.parametrize("kind", ["broadcast", "collect", "fcollect", "alltoall"])
@@ -140,8 +161,9 @@ def test_host_staged_many_chunks(kind):
     L.osgpu_finalize()
     os.environ["OSGPU_STAGE_BYTES"] = "4096"
     try:
-        _run_case(False, kind, 32, (4, 0, 0, 4), 30011, root=3, seed=9)
-        _run_case(False, kind, 64, (8, 1, 1, 3), 9001, root=2, seed=10)
+        with host_path("staged"):
+            _run_case(False, kind, 32, (4, 0, 0, 4), 30011, root=3, seed=9)
+            _run_case(False, kind, 64, (8, 1, 1, 3), 9001, root=2, seed=10)
     finally:
         L.osgpu_finalize()
         del os.environ["OSGPU_STAGE_BYTES"]
@@ -149,11 +171,8 @@ def test_host_staged_many_chunks(kind):
 
 @pytest.mark.parametrize("kind", ["broadcast", "collect", "fcollect", "alltoall"])
 def test_host_getmem_path(kind):
-    os.environ["OSGPU_HOST_PATH"] = "getmem"
-    try:
+    with host_path("getmem"):
         _run_case(False, kind, 64, (3, 0, 0, 3), 3001, root=2, seed=11)
-    finally:
-        del os.environ["OSGPU_HOST_PATH"]
 
 
 def test_collect32_dword_phases_and_byte_path():
