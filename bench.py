@@ -12,7 +12,8 @@ N = 1 (default) -- BASELINE config 2: nreduce = 64 Mi doubles, 1 MI355X,
   B = (K + 1) * nreduce * 8 (2 reads + 1 write), value = steps * B / t.
   Extra fields: roofline (HIP events on the launch stream + PMC traffic from
   profiles/), the full C-API call (2 PEs, timed in C), the host-staged
-  (PCIe-inclusive) rate, the reference's CPU loop shape on this host.
+  (PCIe-inclusive) rate, the data-movement collectives (copy kernel roofline,
+  fcollect64 through the C ABI), the reference's CPU loop shape on this host.
 
 N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   shmem_double_sum_to_all(nreduce = 64 Mi per PE) over all N PEs (weak
@@ -23,8 +24,9 @@ N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   / t (SURVEY.md 8d aggregate: sum over GPUs of the shard-fold bytes), t = the
   max over ranks.  Then, in the same run: RCCL allreduce on the same buffers,
   BASELINE config 4 (nreduce = 1 Gi, RCCL) and config 5 (float min/max/prod,
-  128 Mi per PE, host-resident, H2D/D2H included).  A watchdog prints the
-  line with what has been measured if the run exceeds --deadline seconds.
+  128 Mi per PE, host-resident, H2D/D2H included), and fcollect64 over the
+  device heaps (xGMI), RCCL and host staging.  A watchdog prints the line
+  with what has been measured if the run exceeds --deadline seconds.
 """
 import argparse
 import ctypes
@@ -149,6 +151,22 @@ def host_staged_time(n, reps=5):
     return out
 
 
+def collectives_single(P=4, nb=64 << 20, reps=10):
+    """SURVEY.md 8f row 4 on one GPU (tools/coll_bench.py has the full
+    sweep): the copy kernel alone (P ranges of nb bytes, HIP events; traffic
+    2*P*nb per launch) and shmem_fcollect64 through the C ABI by P
+    threads-as-PEs on this GPU (all-PE traffic 2*P*P*nb per call)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import coll_bench as CB
+    t, bw = CB.kernel_rate(P, nb, reps)
+    out = {"copy_kernel": {"ranges": P, "bytes_per_range": nb, "us": t * 1e6,
+                           "GBps": bw / 1e9, "frac_of_8TBps": bw / 8e12}}
+    t = CB.api_time("fcollect", P, nb, reps, True)
+    out["fcollect64_device"] = {"pes": P, "bytes_per_pe": nb, "ms_per_call": t * 1e3,
+                                "GBps_all_pes": CB.moved("fcollect", P, nb) / t / 1e9}
+    return out
+
+
 def api_call_time(n, reps=20):
     """Full shmem_double_sum_to_all through the C ABI, timed in C
     (tests/support/pe_threads.c:pet_time_to_all): a 2-PE active set, one
@@ -255,6 +273,10 @@ def bench_single(args):
             res["host_staged"] = host_staged_time(n)
         except Exception as e:
             res["host_staged"] = {"error": repr(e)}
+        try:
+            res["collectives"] = collectives_single()
+        except Exception as e:
+            res["collectives"] = {"error": repr(e)}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_n)
     print(json.dumps(res), flush=True)
@@ -314,6 +336,73 @@ def _agree(dist, world, ok):
     allok = [None] * world
     dist.all_gather_object(allok, bool(ok))
     return all(allok)
+
+
+def _block_sums(t, nb, world, torch):
+    """int64 wrap-around sum of each nb-byte block of a uint8 tensor."""
+    return [int(t[i * nb:(i + 1) * nb].view(torch.int64).sum().item()) for i in range(world)]
+
+
+def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_bytes, team_ok,
+                    rccl_ok, args, PES):
+    """shmem_fcollect64 with one PE per GPU.  Every PE's target gathers all
+    contributions: per PE (P-1)/P of the target bytes arrive over xGMI (or
+    PCIe for host memory).  Parity: every nb-byte block of every target has
+    the int64 checksum of the contributing PE's source, all ranks agree."""
+    fc = L.shmem_fcollect64
+    ps = PES.pes_heap(rank) + (1 << 20) - 4096       # symmetric pSync
+    out = {"note": "fcollect64, one PE per GPU; GBps = target bytes gathered per PE / time"}
+
+    def check(src_t, tgt_t, nb):
+        mine = int(src_t[:nb].view(torch.int64).sum().item())
+        allsum = [None] * world
+        dist.all_gather_object(allsum, mine)
+        got = _block_sums(tgt_t, nb, world, torch)
+        return _agree(dist, world, got == allsum)
+
+    nb = (heap_bytes // world) // 256 * 256          # contribution per PE (device)
+    hsrc[:nb].random_(0, 256, generator=torch.Generator(device=dev).manual_seed(500 + rank))
+    torch.cuda.synchronize()
+
+    def stepd():
+        fc(htgt.data_ptr(), hsrc.data_ptr(), nb // 8, 0, 0, world, ps)
+
+    for name, path, usable in (("device_copy_xgmi", osgpu.PATH_P2P, team_ok),
+                               ("rccl_allgather", osgpu.PATH_RCCL, rccl_ok)):
+        if not usable:
+            continue
+        L.osgpu_set_path(path)
+        htgt.zero_()
+        torch.cuda.synchronize()
+        t = _timed(stepd, 3, 1, dist, torch)
+        out[name] = {"bytes_per_pe": nb, "ms_per_call": t / 3 * 1e3,
+                     "GBps_per_pe": 3 * world * nb / t / 1e9,
+                     "xgmi_in_GBps_per_pe": 3 * (world - 1) * nb / t / 1e9,
+                     "bit_exact_blocks": check(hsrc, htgt, nb)}
+    L.osgpu_set_path(osgpu.PATH_AUTO)
+
+    nbh = 64 << 20                                   # host: 64 MiB per PE, pinned
+    hs = torch.empty(nbh, dtype=torch.uint8).pin_memory()
+    ht = torch.empty(world * nbh, dtype=torch.uint8).pin_memory()
+    hs.random_(0, 256, generator=torch.Generator().manual_seed(600 + rank))
+
+    def steph():
+        fc(ht.data_ptr(), hs.data_ptr(), nbh // 8, 0, 0, world, ps)
+
+    old = os.environ.get("OSGPU_HOST_PATH")
+    os.environ["OSGPU_HOST_PATH"] = "staged"
+    try:
+        t = _timed(steph, 3, 1, dist, torch)
+    finally:
+        if old is None:
+            os.environ.pop("OSGPU_HOST_PATH", None)
+        else:
+            os.environ["OSGPU_HOST_PATH"] = old
+    out["host_staged_pinned"] = {"bytes_per_pe": nbh, "ms_per_call": t / 3 * 1e3,
+                                 "GBps_per_pe": 3 * world * nbh / t / 1e9,
+                                 "pcie_GBps_per_pe": 3 * (world + 1) * nbh / t / 1e9,
+                                 "bit_exact_blocks": check(hs, ht, nbh)}
+    return out
 
 
 def bench_multi(args):
@@ -500,6 +589,17 @@ def bench_multi(args):
             _log(rank, "config5 done")
         except Exception as e:
             res["config5"] = {"error": repr(e)[:300]}
+
+    # ---- fcollect64 on the same machinery, one PE per
+    # GPU -- device heaps over xGMI (COPY path), RCCL allgather, host staging
+    if not args.no_extra:
+        state["phase"] = "collectives"
+        try:
+            res["collectives"] = _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc,
+                                                 htgt, n * 8, team_ok, rccl_ok, args, PES)
+            _log(rank, "collectives done")
+        except Exception as e:
+            res["collectives"] = {"error": repr(e)[:300]}
 
     state["phase"] = "teardown"
     emit()
