@@ -7,14 +7,14 @@
  * pthreads as PEs over an in-process heap; a UCX put/get between PEs of one
  * node is a memcpy into/out of the peer's slot (the shared-memory transport),
  * so each collective is restated as the memcpys its reference code issues:
- *   fcollect  src/shmemc/fcollect.c:29-36  every PE puts its source at block
- *             vpe of every target (PE_size puts), barrier (:37)
- *   collect   src/shmemc/collect.c:35-66   offset wavefront through pSync
+ *   fcollect  src/shmemc/fcollect.c:32-38  every PE puts its source at block
+ *             vpe of every target (PE_size puts), barrier (:39)
+ *   collect   src/shmemc/collect.c:32-64   offset wavefront through pSync
  *             (left to right: PE i waits for PE i-1's offset), then PE_size
- *             puts at that offset, barrier (:69)
+ *             puts at that offset, barrier (:68)
  *   broadcast src/shmemc/broadcast.c:29-42 linear: barrier, every non-root
  *             gets the root's source
- *   alltoall  src/alltoall.c:61-84          PE_size gets of one block each
+ *   alltoall  src/alltoall.c:59-82          PE_size gets of one block each
  * Kinds: 0 broadcast, 1 collect, 2 fcollect, 3 alltoall (oracle_coll.py).
  */
 #define _GNU_SOURCE

@@ -43,10 +43,10 @@ def broadcast(sources: dict, targets: dict, nbytes: int, PE_root: int,
 
 def collect(sources: dict, targets: dict, nbytes_of: dict, PE_start: int,
             logPE_stride: int, PE_size: int) -> dict:
-    """src/shmemc/collect.c:28-70: the wavefront gives member i the offset
-    sum(nbytes of members 0..i-1) (:39-54, pSync carries it left to right),
+    """src/shmemc/collect.c:24-69: the wavefront gives member i the offset
+    sum(nbytes of members 0..i-1) (:32-50, pSync carries it left to right),
     then member i puts its nbytes_of[i] source bytes at that offset of every
-    member's target (:57-66): every target = concatenation in active-set
+    member's target (:52-64): every target = concatenation in active-set
     order."""
     pes = active_set(PE_start, logPE_stride, PE_size)
     cat = np.concatenate([sources[pe][:nbytes_of[pe]] for pe in pes]) if pes else \
@@ -59,9 +59,9 @@ def collect(sources: dict, targets: dict, nbytes_of: dict, PE_start: int,
 
 def fcollect(sources: dict, targets: dict, nbytes: int, PE_start: int,
              logPE_stride: int, PE_size: int) -> dict:
-    """src/shmemc/fcollect.c:25-38: member vpe = (me - PE_start) >>
-    logPE_stride puts its nbytes at tidx = nbytes * vpe of every member's
-    target (:31-35)."""
+    """src/shmemc/fcollect.c:19-40: member vpe = (me - PE_start) >>
+    logPE_stride (:27) puts its nbytes at tidx = nbytes * vpe (:28) of every
+    member's target (:32-38)."""
     pes = active_set(PE_start, logPE_stride, PE_size)
     return collect(sources, targets, {pe: nbytes for pe in pes}, PE_start, logPE_stride,
                    PE_size)
@@ -69,12 +69,12 @@ def fcollect(sources: dict, targets: dict, nbytes: int, PE_start: int,
 
 def alltoall(sources: dict, targets: dict, nbytes: int, PE_start: int,
              logPE_stride: int, PE_size: int, block_index: str = "active_set") -> dict:
-    """src/alltoall.c:61-84: for the i-th member pe, me gets nbytes from
-    pe's source at sidx into its target at tidx = nbytes * i (:70-76).
+    """src/alltoall.c:59-82: for the i-th member pe, me gets nbytes from
+    pe's source at sidx into its target at tidx = nbytes * i (:74-81).
 
     block_index="active_set" (the OpenSHMEM 1.4 definition, this
     implementation): sidx = nbytes * (me's active-set index).
-    block_index="rank" (the reference's literal code, :71 `sidx = _size *
+    block_index="rank" (the reference's literal code, :76 `sidx = _size *
     nelems * proc.rank`): sidx = nbytes * me.  The two agree whenever
     PE_start = 0 and logPE_stride = 0."""
     pes = active_set(PE_start, logPE_stride, PE_size)

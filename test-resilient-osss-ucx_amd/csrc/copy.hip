@@ -4,7 +4,7 @@
 // mapped into this process, copied by ONE launch.
 //
 // The reference moves these bytes with shmemc_put / shmemc_get over UCX
-// (src/shmemc/fcollect.c:29-35, src/shmemc/collect.c:57-66,
+// (src/shmemc/fcollect.c:32-38, src/shmemc/collect.c:52-64,
 // src/shmemc/broadcast.c:39-41).  Here the owner of every target pulls all
 // its pieces with 16-byte streaming loads: HBM-bound on one GPU, xGMI-bound
 // across GPUs; 2 bytes of traffic (read + write) per byte copied.

@@ -7,14 +7,14 @@
 //   broadcast  src/shmemc/broadcast.c:29-42 (linear: barrier, every non-root
 //              gets the root's source; the tree/binomial variants :48-250
 //              forward it) -- the root's own target is never written;
-//   collect    src/shmemc/collect.c:28-70: an offset wavefront through pSync
+//   collect    src/shmemc/collect.c:24-69: an offset wavefront through pSync
 //              (each PE learns the sum of its left neighbours' nelems), then
 //              every PE puts its source at that offset of every target,
 //              barrier;
-//   fcollect   src/shmemc/fcollect.c:25-38: every PE puts its source at
-//              block vpe = (me - PE_start) >> logPE_stride of every target,
-//              barrier;
-//   alltoall   src/alltoall.c:61-84: block i of my target <- a block of PE
+//   fcollect   src/shmemc/fcollect.c:19-40: every PE puts its source at
+//              block vpe = (me - PE_start) >> logPE_stride (:27) of every
+//              target (:32-38), barrier (:39);
+//   alltoall   src/alltoall.c:59-82: block i of my target <- a block of PE
 //              i's source (gets, no synchronisation at all).
 //
 // Here every PE PULLS all the pieces of its own target in one launch of
@@ -37,7 +37,7 @@
 // it in a spare pSync word (the reference's barrier uses pSync[0] only,
 // src/shmemc/barrier.c:64-97), reads its peers' with shmem_getmem after the
 // first barrier and clears its word after the last -- pSync is returned at
-// SHMEM_SYNC_VALUE, as the reference's wavefront leaves it (collect.c:68).
+// SHMEM_SYNC_VALUE, as the reference's wavefront leaves it (collect.c:67).
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
