@@ -6,10 +6,16 @@ rank, shmem_barrier = dist.barrier.
 modes
   host  no GPU: fold order, shard partition and the nreduce = 0 collective
         (two barriers through the Python callback) -- checked across ranks
+  hostcoll  no GPU, shared-memory PE runtime: every data-movement
+        collective with nelems = 0 (synchronises only, pSync left zeroed)
   ipc   GPU: each rank allocates its device symmetric heap, exports it with
         osgpu_ipc_get_handle, opens every peer's (osgpu_ipc_open) and
         registers them; then shmem_<T>_<op>_to_all runs on the team path,
-        the pull path and in place, results written for the parent to check
+        the pull path and in place, and the collectives (broadcast / collect /
+        fcollect / alltoall) on the COPY path; results written for the
+        parent to check
+  hoststaged  GPU, host heaps in shared memory: reductions and collectives
+        on the STAGED and GETMEM paths
 usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. \
        python mp_worker.py MODE OUTDIR
 """
@@ -49,13 +55,35 @@ def pe_ops(rank, world, counter):
     return ops, (my_pe, n_pes, barrier)
 
 
+def run_colls(L, rank, world, src_addr, tgt_addr, psync, out, tag, write, read):
+    """Every case of support/coll_cases.py: source at src_addr, target
+    (sentinel-filled) at tgt_addr, both symmetric; target bytes to `out`."""
+    from support import coll_cases as CC
+    for kind, bits, counts, root in CC.cases(world):
+        raw = CC.source(kind, bits, counts, rank, world)
+        tb = CC.target_bytes(kind, bits, counts, world)
+        if raw.size:
+            write(src_addr, raw)
+        write(tgt_addr, np.full(tb, CC.SENTINEL, np.uint8))
+        dist.barrier()
+        f = osgpu.coll(kind, bits)
+        if kind == "broadcast":
+            f(tgt_addr, src_addr, counts[rank], root, 0, 0, world, psync)
+        else:
+            f(tgt_addr, src_addr, counts[rank], 0, 0, world, psync)
+        out[CC.key(kind, bits, tag)] = bytes(read(tgt_addr, tb)).hex()
+        assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
+        dist.barrier()
+
+
 def main():
     mode, outdir = sys.argv[1], sys.argv[2]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     L = osgpu.load()
     counter = [0]
-    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode == "hoststaged":
+    PES = None
+    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in ("hoststaged", "hostcoll"):
         from support import peshm
         PES = peshm.init(rank, world, 1 << 24, dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -89,7 +117,25 @@ def main():
                 out[f"{t}/{op}/{hp}/{int(inplace)}"] = got.tobytes().hex()
                 assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
                 dist.barrier()
+        for hp in ("staged", "getmem"):
+            os.environ["OSGPU_HOST_PATH"] = hp
+            run_colls(L, rank, world, base, base + (1 << 22), psync, out, hp,
+                      lambda off, raw: ctypes.memmove(off, raw.ctypes.data, raw.size),
+                      lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
+        os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
+    if mode == "hostcoll":
+        psync = PES.pes_heap(rank) + (1 << 24) - 4096
+        buf = PES.pes_heap(rank)
+        for kind in ("broadcast", "collect", "fcollect", "alltoall"):
+            for bits in (32, 64):
+                f = osgpu.coll(kind, bits)
+                if kind == "broadcast":
+                    f(buf, buf, 0, world - 1, 0, 0, world, psync)
+                else:
+                    f(buf, buf, 0, 0, 0, world, psync)
+                assert not any(ctypes.string_at(psync, 512)), "pSync not reset"
+        res["zero_byte_collectives"] = "ok"
     if mode == "host":
         res["order"] = osgpu.fold_order(rank, 0, 0, world)
         res["shards"] = {str(eb): [osgpu.shard_range(n, world, rank, eb)
@@ -144,6 +190,21 @@ def main():
                 out[f"{t}/{op}/{path}/{int(inplace)}"] = got.tobytes().hex()
                 dist.barrier()
         L.osgpu_set_path(osgpu.PATH_AUTO)
+        if PES is not None:  # collect needs the runtime's getmem (pSync words)
+            psync = PES.pes_heap(rank) + (1 << 24) - 4096
+
+            def wr(off, raw):
+                lo = off - heap.data_ptr()
+                heap[lo:lo + raw.size].copy_(torch.from_numpy(raw.copy()).cuda())
+                torch.cuda.synchronize()
+
+            def rd(off, nb):
+                torch.cuda.synchronize()
+                lo = off - heap.data_ptr()
+                return heap[lo:lo + nb].cpu().numpy()
+
+            run_colls(L, rank, world, heap.data_ptr(), heap.data_ptr() + (1 << 21), psync, out,
+                      "device", wr, rd)
         res["out"] = out
         dist.barrier()
         for p in mapped:

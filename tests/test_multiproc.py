@@ -65,6 +65,26 @@ def test_host_logic_world2(tmp_path):
     assert [r["barriers"] for r in res] == [2, 2]
 
 
+def test_zero_byte_collectives_processes(tmp_path):
+    """broadcast/collect/fcollect/alltoall with nelems = 0, one process per
+    PE over the shared-memory runtime, no GPU: only synchronisation."""
+    res = launch("hostcoll", 2, tmp_path)
+    assert [r["zero_byte_collectives"] for r in res] == ["ok", "ok"]
+
+
+def _check_colls(res, tag):
+    from support import coll_cases as CC
+    world = len(res)
+    n = 0
+    for kind, bits, counts, root in CC.cases(world):
+        want = CC.expected(kind, bits, counts, root, world)
+        for r in range(world):
+            assert res[r]["out"][CC.key(kind, bits, tag)] == want[r].tobytes().hex(), \
+                (kind, bits, tag, r)
+            n += 1
+    assert n == 8 * world
+
+
 def _check_specs(res, specs, seed):
     for t, op, n, d in specs:
         src = [O.gen_input(t, n, O.pe_seed(seed, r), d) for r in range(len(res))]
@@ -89,6 +109,8 @@ def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
              ("int", "prod", 1000, "bits"), ("complexd", "prod", 999, "edge"),
              ("longdouble", "sum", 517, "wide"), ("short", "xor", 4096, "bits"))
     _check_specs(res, specs, 0xABC)
+    if pes == "shm":  # collect needs getmem: the shm runtime has it
+        _check_colls(res, "device")
 
 
 @pytest.mark.gpu
@@ -107,4 +129,6 @@ def test_host_staged_processes(tmp_path, world, monkeypatch):
              ("long", "or", 65, "or"), ("complexf", "prod", 1000, "edge"),
              ("longdouble", "min", 333, "edge"))
     _check_specs(res, specs, 0xDEF)
+    _check_colls(res, "staged")
+    _check_colls(res, "getmem")
 
