@@ -51,6 +51,35 @@ struct CopySeg {
 };
 hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
 
+// One-launch reduce-to-all for small calls (fused.hip): the call's two
+// barriers run inside the kernel as epoch flags in every member's flag area
+// (uncached device memory, mapped into every member).  Word layout of a
+// flag area (unsigned long long):
+constexpr int kFlagArrive = 0;    // [0, 8): arrive[member]
+constexpr int kFlagDone = 8;      // [8, 16): done[member]
+constexpr int kFlagTicket = 16;   // last-workgroup ticket (u32)
+constexpr int kFlagWords = 32;
+// fused grids: at most one workgroup of 256 lanes per CU of the GPU (256 on
+// MI355X), split between the members sharing it (one member per GPU: all)
+constexpr int kFusedBlocksPerGpu = 256;
+struct FusedArgs {
+    const void *src[kMaxTeam];            // every member's source, active-set order
+    void *dst[kMaxTeam];                  // outputs: team form every member's target, pull form mine
+    int q[kMaxTeam];                      // active-set index whose fold order dst[d] uses
+    unsigned long long *flags[kMaxTeam];  // every member's flag area
+    unsigned long long *mine;             // my flag area
+    int *err;                             // host-mapped: 1 arrive / 2 done timed out
+    unsigned long long *done_host;        // host-mapped: epoch, written once the call is complete
+    unsigned long long epoch, timeout;    // timeout in wall-clock ticks
+    size_t n;                             // elements from src[p] / dst[d]
+    size_t nvec, head, tail_start;        // filled by launch_fused
+    int nedge, P, D, me;                  // me: my active-set index
+    int max_blocks;                       // grid cap (co-residency on a shared GPU)
+    unsigned long long *trace;            // optional host-mapped phase clock (8 words)
+};
+bool fused_supported(int type);
+hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s);
+
 // x87 80-bit extended combine (soft-float on the GPU), longdouble.hip
 hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, size_t n,
                              hipStream_t s);

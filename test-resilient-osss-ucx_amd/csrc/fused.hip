@@ -1,0 +1,325 @@
+// fused.hip -- one launch per small reduce-to-all call: the two barriers of
+// the reference (src/reductions.c:82 and :113, the AMO tree barrier of
+// src/shmemc/barrier.c:64-97 on pSync[0]) become epoch flags in device
+// memory, written over xGMI (or inside one GPU) by the kernel itself.
+//
+// Why: a small call on the host-barrier path costs a launch, a completion
+// wait and two host barriers (~25-30 us for 1 Ki ints); the
+// compute is noise.  Here the host enqueues ONE kernel and waits once.
+//
+// Per active set every member PE owns a flag area (uncached device memory,
+// IPC-mapped into every member, runtime.cpp sync_setup):
+//   words [0, 8)   arrive[i]: epoch of the last call member i entered
+//   words [8, 16)  done[i]:   epoch of the last call member i finished
+//   word  16       ticket:    last-workgroup election inside one launch
+// Epochs grow by one per fused call on the set, so nothing is ever reset
+// (pSync stays at SHMEM_SYNC_VALUE, untouched).
+//
+// Protocol of one launch (member `me`, epoch E):
+//  1. workgroup 0, lanes i < P: arrive[me] := E in member i's area;
+//  2. every workgroup: one lane waits until all P arrive[] words of MY area
+//     are >= E (every source ready, every target writable);
+//  3. the combine body (grid-stride): team form -- shard of every member's
+//     target, each in that member's fold order -- or pull form -- my own
+//     target over all n;
+//  4. every workgroup: system-scope release, then (grids of more than one
+//     workgroup) a ticket; the last one
+//     writes done[me] := E into every member's area and waits until all P
+//     done[] words of my area are >= E (every peer finished writing my
+//     target and reading my source), then stores E to a host-mapped word the
+//     calling thread spins on -- it returns without waiting for the launch
+//     to retire (the launch-to-completion notification is most of the
+//     latency of a small call).
+// Waits are bounded (wall clock); a timeout sets a host-mapped error word,
+// which the host turns into a fatal error, and the grid still drains.
+//
+// Co-residency: step 2 needs every member's workgroup 0 to run while my
+// workgroups wait.  Members on other GPUs always make progress; members
+// sharing my GPU (separate processes: threads of one process share its few
+// hardware queues and are refused in runtime.cpp) split the GPU's 256 CUs,
+// one workgroup of 256 lanes per CU, so every member's grid is resident at
+// once (FusedArgs::max_blocks).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <type_traits>
+
+#include "combine.hpp"
+#include "elem_ops.hpp"
+
+#pragma clang fp contract(off)
+
+namespace osgpu {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kFBlock = 256;
+
+template <typename T>
+union FVec {
+    u32x4 v;
+    T e[16 / sizeof(T)];
+};
+
+__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void st_sys(unsigned long long *p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Results are stored system-coherent (write-through, sc0 sc1): they leave no
+// dirty L2 line for the completion fence to write back.  Measured at 1 MiB
+// per PE, 2 processes on one GPU: fence 7.4 us with nontemporal stores and a
+// fence per wave, 4.2 us with one fence per workgroup, 2.7 us write-through.
+__device__ __forceinline__ void store_out(u32x4 *p, u32x4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// one lane: wait until f[0..P) >= epoch; false (and the error word set) on timeout
+__device__ bool wait_epoch(const unsigned long long *f, int P, unsigned long long epoch,
+                           unsigned long long timeout, int *err, int code)
+{
+    const unsigned long long t0 = (unsigned long long) wall_clock64();
+    for (int j = 0; j < P; j++) {
+        while (ld_sys(f + j) < epoch) {
+            if ((unsigned long long) wall_clock64() - t0 > timeout) {
+                __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return true;
+}
+
+// D outputs of one element: output d belongs to member q[d] and folds
+// x[q[d]] first, then the others ascending (src/reductions.c:79-111).
+// Integer ops are order-independent: fold once.
+template <typename T, int OP>
+__device__ __forceinline__ void fold_outputs(const T (&x)[kMaxTeam], int P, int D,
+                                             const int (&q)[kMaxTeam], T (&r)[kMaxTeam])
+{
+    if (std::is_integral<T>::value) {
+        T acc = x[0];
+#pragma unroll
+        for (int j = 1; j < kMaxTeam; j++)
+            if (j < P) acc = Elem<T, OP>::f(acc, x[j]);
+#pragma unroll
+        for (int d = 0; d < kMaxTeam; d++) r[d] = acc;
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < kMaxTeam; d++) {
+        if (d >= D) break;
+        const int o = q[d];
+        T acc = x[0];
+#pragma unroll
+        for (int j = 0; j < kMaxTeam; j++)
+            if (j == o) acc = x[j];
+#pragma unroll
+        for (int j = 0; j < kMaxTeam; j++)
+            if (j < P && j != o) acc = Elem<T, OP>::f(acc, x[j]);
+        r[d] = acc;
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void do_elem(const FusedArgs &a, size_t i)
+{
+    const T *const *src = reinterpret_cast<const T *const *>(a.src);
+    T x[kMaxTeam], r[kMaxTeam];
+#pragma unroll
+    for (int j = 0; j < kMaxTeam; j++)
+        x[j] = j < a.P ? src[j][i] : T();
+    fold_outputs<T, OP>(x, a.P, a.D, a.q, r);
+#pragma unroll
+    for (int d = 0; d < kMaxTeam; d++)
+        if (d < a.D) static_cast<T *>(a.dst[d])[i] = r[d];
+}
+
+template <typename T, int OP, bool VEC>
+__global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
+{
+    __shared__ int s_go;
+    const bool tr = a.trace && blockIdx.x == 0 && threadIdx.x == 0;
+    if (tr) a.trace[0] = (unsigned long long) wall_clock64();
+    // 1. arrive (src/reductions.c:82 -- my source is ready, my target free)
+    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
+        st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
+    // 2. wait for every member's arrival
+    if (threadIdx.x == 0)
+        s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
+    __syncthreads();
+    if (!s_go) return;
+    if (tr) a.trace[1] = (unsigned long long) wall_clock64();
+
+    // 3. combine body
+    if (VEC) {
+        constexpr int W = 16 / sizeof(T);
+        if (blockIdx.x == 0 && (int) threadIdx.x < a.nedge) {
+            const size_t e =
+                threadIdx.x < a.head ? threadIdx.x : a.tail_start + (threadIdx.x - a.head);
+            do_elem<T, OP>(a, e);
+        }
+        const size_t stride = (size_t) gridDim.x * kFBlock;
+        for (size_t j = (size_t) blockIdx.x * kFBlock + threadIdx.x; j < a.nvec; j += stride) {
+            FVec<T> in[kMaxTeam];
+#pragma unroll
+            for (int p = 0; p < kMaxTeam; p++)
+                if (p < a.P)
+                    in[p].v = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4 *>(static_cast<const T *>(a.src[p]) +
+                                                        a.head) + j);
+            FVec<T> out[kMaxTeam];
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                T x[kMaxTeam], r[kMaxTeam];
+#pragma unroll
+                for (int p = 0; p < kMaxTeam; p++) x[p] = p < a.P ? in[p].e[w] : T();
+                fold_outputs<T, OP>(x, a.P, a.D, a.q, r);
+#pragma unroll
+                for (int d = 0; d < kMaxTeam; d++) out[d].e[w] = r[d];
+            }
+#pragma unroll
+            for (int d = 0; d < kMaxTeam; d++)
+                if (d < a.D)
+                    store_out(reinterpret_cast<u32x4 *>(static_cast<T *>(a.dst[d]) + a.head) + j,
+                              out[d].v);
+        }
+    } else {
+        const size_t stride = (size_t) gridDim.x * kFBlock;
+        for (size_t i = (size_t) blockIdx.x * kFBlock + threadIdx.x; i < a.n; i += stride)
+            do_elem<T, OP>(a, i);
+    }
+
+    // 4. completion (src/reductions.c:113): my stores and reads are done.
+    // Every wave waits for its own stores, then ONE lane per workgroup makes
+    // them visible system-wide (an L2 writeback per fence: one per workgroup,
+    // not one per wave) and takes a ticket; the last workgroup signals.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (tr) a.trace[2] = (unsigned long long) wall_clock64();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        s_go = 1;
+        if (gridDim.x > 1) {
+            unsigned *ticket = reinterpret_cast<unsigned *>(a.mine + kFlagTicket);
+            const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            s_go = t == gridDim.x - 1;
+            if (s_go) {
+                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            }
+        }
+        if (tr) a.trace[3] = (unsigned long long) wall_clock64();
+        if (s_go) {
+            if (a.trace) a.trace[4] = a.trace[5] = (unsigned long long) wall_clock64();
+            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
+            if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2)) {
+                if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
+                // the host returns on this word, without waiting for the launch to retire
+                __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
+template <typename T, int OP>
+hipError_t fused_launch_t(FusedArgs a, hipStream_t s)
+{
+    constexpr int W = 16 / sizeof(T);
+    const uintptr_t phase = (uintptr_t) a.src[0] & 15;
+    bool vec = (phase % sizeof(T)) == 0;
+    for (int p = 0; p < a.P; p++) vec = vec && (((uintptr_t) a.src[p] & 15) == phase);
+    for (int d = 0; d < a.D; d++) vec = vec && (((uintptr_t) a.dst[d] & 15) == phase);
+    size_t work;
+    if (vec) {
+        size_t head = phase ? (16 - phase) / sizeof(T) : 0;
+        if (head > a.n) head = a.n;
+        a.head = head;
+        a.nvec = (a.n - head) / W;
+        a.tail_start = head + a.nvec * W;
+        a.nedge = (int) (head + (a.n - a.tail_start));
+        work = a.nvec;
+    } else {
+        a.head = a.nvec = a.tail_start = 0;
+        a.nedge = 0;
+        work = a.n;
+    }
+    size_t blocks = (work + kFBlock - 1) / kFBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (size_t) a.max_blocks) blocks = (size_t) a.max_blocks;
+    if (vec)
+        hipLaunchKernelGGL((fused_kernel<T, OP, true>), dim3((unsigned) blocks), dim3(kFBlock), 0,
+                           s, a);
+    else
+        hipLaunchKernelGGL((fused_kernel<T, OP, false>), dim3((unsigned) blocks), dim3(kFBlock),
+                           0, s, a);
+    return hipGetLastError();
+}
+
+#define FUSED_CASE(OPC)                                                        \
+    case OPC: return fused_launch_t<T, OPC>(a, s);
+
+template <typename T>
+hipError_t fused_int(int op, const FusedArgs &a, hipStream_t s)
+{
+    switch (op) {
+        FUSED_CASE(OP_SUM) FUSED_CASE(OP_PROD) FUSED_CASE(OP_AND) FUSED_CASE(OP_OR)
+        FUSED_CASE(OP_XOR) FUSED_CASE(OP_MAX) FUSED_CASE(OP_MIN)
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t fused_real(int op, const FusedArgs &a, hipStream_t s)
+{
+    switch (op) {
+        FUSED_CASE(OP_SUM) FUSED_CASE(OP_PROD) FUSED_CASE(OP_MAX) FUSED_CASE(OP_MIN)
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t fused_cplx(int op, const FusedArgs &a, hipStream_t s)
+{
+    switch (op) {
+        FUSED_CASE(OP_SUM) FUSED_CASE(OP_PROD)
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+bool fused_supported(int type) { return type != T_LONGDOUBLE && type >= 0 && type < T_NTYPES; }
+
+hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s)
+{
+    if (a.P < 2 || a.P > kMaxTeam || a.D < 1 || a.D > kMaxTeam || a.me < 0 || a.me >= a.P ||
+        a.max_blocks < 1 || a.max_blocks > kFusedBlocksPerGpu)
+        return hipErrorInvalidValue;
+    switch (type) {
+    case T_SHORT: return fused_int<int16_t>(op, a, s);
+    case T_INT: return fused_int<int32_t>(op, a, s);
+    case T_LONG:
+    case T_LONGLONG: return fused_int<int64_t>(op, a, s);
+    case T_FLOAT: return fused_real<float>(op, a, s);
+    case T_DOUBLE: return fused_real<double>(op, a, s);
+    case T_COMPLEXF: return fused_cplx<cfloat>(op, a, s);
+    case T_COMPLEXD: return fused_cplx<cdouble>(op, a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace osgpu

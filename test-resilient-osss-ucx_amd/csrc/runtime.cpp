@@ -74,13 +74,60 @@ int env_choice(const char *var, const char *alt, int def_is_alt)
     return strcmp(e, alt) == 0;
 }
 
-// Entry: device work this process enqueued earlier (on any stream) may still
-// be producing `source`; the collective reads it only after it is done.
-// OSGPU_ENTRY_SYNC=none skips this for callers that synchronise themselves.
-void entry_sync(const char *where)
+// Entry: device work this process enqueued earlier may still be producing
+// `source`; the collective reads it only after it is done.  OSGPU_ENTRY_SYNC:
+//   stream (default)  hipStreamSynchronize of the legacy default stream,
+//                     which waits for every blocking stream too (PyTorch's
+//                     default stream is that stream); producer work on the
+//                     caller's own non-blocking streams is the caller's to
+//                     order, as with CUDA-aware MPI;
+//   device            hipDeviceSynchronize: every stream of the process,
+//                     including this PE's own, whose last fused launch may
+//                     still be retiring (~15 us after its completion word);
+//   spin              device, after spinning until this PE's stream is idle;
+//   none              the caller orders its own producer work.
+int entry_mode()
 {
-    static const int skip = env_choice("OSGPU_ENTRY_SYNC", "none", 0);
-    if (!skip) HIPCHK(where, hipDeviceSynchronize());
+    static const int m = [] {
+        const char *e = getenv("OSGPU_ENTRY_SYNC");
+        if (!e || !strcmp(e, "stream")) return ENTRY_STREAM;
+        if (!strcmp(e, "device")) return ENTRY_DEVICE;
+        if (!strcmp(e, "spin")) return ENTRY_SPIN;
+        if (!strcmp(e, "none")) return ENTRY_NONE;
+        return ENTRY_STREAM;
+    }();
+    return m;
+}
+
+static void spin_idle(const char *where, hipStream_t st)
+{
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+    if (e != hipSuccess) fatal(where, "stream: %s", hipGetErrorString(e));
+}
+
+// host-side entry wait (paths whose first barrier is a host barrier)
+void entry_sync(const char *where, hipStream_t own)
+{
+    switch (entry_mode()) {
+    case ENTRY_SPIN:
+        if (own) spin_idle(where, own);
+        HIPCHK(where, hipDeviceSynchronize());
+        break;
+    case ENTRY_DEVICE: HIPCHK(where, hipDeviceSynchronize()); break;
+    case ENTRY_STREAM: HIPCHK(where, hipStreamSynchronize(nullptr)); break;
+    }
+}
+
+// Entry ordering of a launch on `st` whose barriers run on the device (the
+// fused path).  The same waits as entry_sync; in `stream` mode they never
+// include this PE's own (non-blocking) stream, whose previous launch may
+// still be retiring after its host-visible completion word was written
+// (measured ~15 us; a GPU-side event wait on the default stream measured
+// slower still, ~55 us per call).
+void entry_order(const char *where, hipStream_t st)
+{
+    entry_sync(where, st);
 }
 
 // Completion of our own stream: hipStreamSynchronize (default; measured
@@ -397,6 +444,76 @@ long pci_key(int dev)
     return ((long) dom << 16 | (long) bus << 8 | d) + 1;
 }
 
+// Publish `local` (a device allocation of `bytes`) to every member of the
+// active set through spare pSync words and map every member's allocation:
+// same process -> raw pointer, other processes -> HIP IPC.  Collective (three
+// barriers); every member returns the same verdict.  pSync is returned zeroed.
+bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &peer,
+                 std::vector<void *> &opened, int *ndev, bool distinct_processes,
+                 int *max_share)
+{
+    int dev = 0;
+    HIPCHK(c.name, hipGetDevice(&dev));
+    StageMsg *mine = reinterpret_cast<StageMsg *>(c.pSync + kPsyncBase);
+    memset(mine, 0, sizeof(*mine));
+    hipIpcMemHandle_t h;
+    if (local && hipIpcGetMemHandle(&h, local) == hipSuccess) memcpy(mine->handle, &h, sizeof(h));
+    else (void) hipGetLastError();
+    mine->raw_ptr = (long) (uintptr_t) local;
+    mine->pid = (long) getpid();
+    mine->slot = local ? (long) bytes : -1;
+    mine->pci = pci_key(dev);
+    barrier(c);
+    bool ok = local != nullptr;
+    peer.assign(c.PE_size, nullptr);
+    std::vector<long> pcis(1, mine->pci), all_pci(1, mine->pci);
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        if (pe == c.me) {
+            peer[i] = local;
+            continue;
+        }
+        StageMsg m;
+        c.ops.getmem(&m, mine, sizeof(m), pe);
+        all_pci.push_back(m.pci);
+        if (std::find(pcis.begin(), pcis.end(), m.pci) == pcis.end()) pcis.push_back(m.pci);
+        if (m.slot != (long) bytes) {
+            ok = false;
+        } else if (m.pid == (long) getpid()) {
+            peer[i] = (char *) (uintptr_t) m.raw_ptr;   // same process (threads as PEs)
+            if (distinct_processes) ok = false;
+        } else {
+            hipIpcMemHandle_t ph;
+            memcpy(&ph, m.handle, sizeof(ph));
+            void *p = nullptr;
+            if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
+                peer[i] = (char *) p;
+                opened.push_back(p);
+            } else {
+                (void) hipGetLastError();
+                ok = false;
+            }
+        }
+    }
+    mine->status = ok ? 1 : 2;
+    barrier(c);
+    bool all_ok = ok;
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        if (pe == c.me) continue;
+        long st = 0;
+        c.ops.getmem(&st, &mine->status, sizeof(long), pe);
+        all_ok = all_ok && st == 1;
+    }
+    barrier(c);
+    memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
+    if (ndev) *ndev = (int) pcis.size();
+    if (max_share) {
+        int mx = 0;
+        for (long k : pcis) mx = std::max(mx, (int) std::count(all_pci.begin(), all_pci.end(), k));
+        *max_share = mx;
+    }
+    return all_ok;
+}
+
 StageSet *stage_setup(const Coll &c)
 {
     int dev = 0;
@@ -417,57 +534,83 @@ StageSet *stage_setup(const Coll &c)
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_in[s], hipEventDisableTiming));
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_out[s], hipEventDisableTiming));
     }
-    StageMsg *mine = reinterpret_cast<StageMsg *>(c.pSync + kPsyncBase);
-    memset(mine, 0, sizeof(*mine));
-    hipIpcMemHandle_t h;
-    if (hipIpcGetMemHandle(&h, S.local) == hipSuccess) memcpy(mine->handle, &h, sizeof(h));
-    else (void) hipGetLastError();
-    mine->raw_ptr = (long) (uintptr_t) S.local;
-    mine->pid = (long) getpid();
-    mine->slot = (long) S.slot;
-    mine->pci = pci_key(dev);
-    barrier(c);
-    bool ok = true;
-    S.peer.assign(c.PE_size, nullptr);
-    std::vector<long> pcis(1, mine->pci);
-    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
-        if (pe == c.me) {
-            S.peer[i] = S.local;
-            continue;
-        }
-        StageMsg m;
-        c.ops.getmem(&m, mine, sizeof(m), pe);
-        if (std::find(pcis.begin(), pcis.end(), m.pci) == pcis.end()) pcis.push_back(m.pci);
-        if ((size_t) m.slot != S.slot) {
-            ok = false;
-        } else if (m.pid == (long) getpid()) {
-            S.peer[i] = (char *) (uintptr_t) m.raw_ptr;   // same process (threads as PEs)
-        } else {
-            hipIpcMemHandle_t ph;
-            memcpy(&ph, m.handle, sizeof(ph));
-            void *p = nullptr;
-            if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
-                S.peer[i] = (char *) p;
-                S.opened.push_back(p);
-            } else {
-                (void) hipGetLastError();
-                ok = false;
-            }
-        }
+    S.ok = map_members(c, S.local, S.slot, S.peer, S.opened, &S.ndev, false, nullptr);
+    return S.ok ? &S : nullptr;
+}
+
+long long g_fused_max = -1;  // -1: from the environment
+
+size_t fused_max_bytes()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_fused_max < 0) {
+        const char *e = getenv("OSGPU_FUSED_MAX_BYTES");
+        g_fused_max = e ? strtoll(e, nullptr, 0) : (1LL << 20);
+        if (g_fused_max < 0) g_fused_max = 0;
     }
-    mine->status = ok ? 1 : 2;
-    barrier(c);
-    bool all_ok = ok;
-    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
-        if (pe == c.me) continue;
-        long st = 0;
-        c.ops.getmem(&st, &mine->status, sizeof(long), pe);
-        all_ok = all_ok && st == 1;
+    return (size_t) g_fused_max;
+}
+
+// ---------------------------------------------------------------------
+// Device-side barriers of the fused small-call path (fused.hip): one flag
+// area per member and active set, in uncached device memory (remote writes
+// over xGMI are seen by a polling load without cache maintenance), mapped
+// into every member like the staging above.
+// ---------------------------------------------------------------------
+
+std::map<std::tuple<int, int, int, int, int>, SyncSet> g_sync;  // (me, set, device)
+
+SyncSet *sync_setup(const Coll &c)
+{
+    int dev = 0;
+    HIPCHK(c.name, hipGetDevice(&dev));
+    auto key = std::make_tuple(c.me, c.PE_start, c.step, c.PE_size, dev);
+    std::unique_lock<std::mutex> lk(g_mu);
+    auto it = g_sync.find(key);
+    if (it != g_sync.end()) return it->second.ok ? &it->second : nullptr;
+    SyncSet &S = g_sync[key];
+    lk.unlock();
+    S.idx = c.index_of(c.me);
+    const size_t bytes = osgpu::kFlagWords * sizeof(unsigned long long);
+    void *p = nullptr;
+    bool ok = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess;
+    if (!ok) (void) hipGetLastError();
+    if (ok && hipMemset(p, 0, bytes) != hipSuccess) ok = false;
+    if (ok && hipHostMalloc((void **) &S.err_h, sizeof(int) * 16,
+                            hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        ok = false;
+    if (ok) {  // word 0: error code; words 8..9: completion epoch
+        memset(S.err_h, 0, sizeof(int) * 16);
+        S.done_h = reinterpret_cast<unsigned long long *>(S.err_h + 8);
+        ok = hipHostGetDevicePointer((void **) &S.err_d, S.err_h, 0) == hipSuccess;
+        S.done_d = reinterpret_cast<unsigned long long *>(S.err_d + 8);
     }
-    barrier(c);
-    memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
-    S.ndev = (int) pcis.size();
-    S.ok = all_ok;
+    int rate_khz = 0;
+    if (ok) ok = hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) ==
+                 hipSuccess && rate_khz > 0;
+    if (!ok) (void) hipGetLastError();
+    if (ok) HIPCHK(c.name, hipDeviceSynchronize());  // zeroed before anyone can write
+    S.local = (unsigned long long *) p;
+    std::vector<char *> peer;
+    // members must be separate processes: PEs that are threads of one process
+    // share its few hardware queues, where one member's spinning kernel can
+    // sit in front of another member's (no co-residency, a deadlock)
+    int share = c.PE_size;
+    ok = map_members(c, ok ? (char *) p : nullptr, bytes, peer, S.opened, nullptr, true, &share);
+    // every member's workgroups must fit on a shared GPU at once (see fused.hip)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 0;
+    (void) hipGetLastError();
+    cus = std::min(std::max(cus, 1), osgpu::kFusedBlocksPerGpu);
+    S.max_blocks = std::max(1, cus / (share > 0 ? share : c.PE_size));
+    S.peer.resize(peer.size());
+    for (size_t i = 0; i < peer.size(); i++) S.peer[i] = (unsigned long long *) peer[i];
+    const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
+    const double secs = e ? atof(e) : 10.0;
+    S.timeout = (unsigned long long) (secs * 1e3 * rate_khz);
+    S.timeout_s = secs;
+    S.ok = ok;
     return S.ok ? &S : nullptr;
 }
 
@@ -616,6 +759,8 @@ int osgpu_rccl_finalize(void)
 
 int osgpu_finalize(void)
 {
+    // fused launches may still be retiring after their calls returned
+    (void) hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto &kv : g_stage) {
         StageSet &S = kv.second;
@@ -630,6 +775,13 @@ int osgpu_finalize(void)
         if (S.st_out) (void) hipStreamDestroy(S.st_out);
     }
     g_stage.clear();
+    for (auto &kv : g_sync) {
+        SyncSet &S = kv.second;
+        for (void *p : S.opened) (void) hipIpcCloseMemHandle(p);
+        if (S.local) (void) hipFree(S.local);
+        if (S.err_h) (void) hipHostFree(S.err_h);
+    }
+    g_sync.clear();
     for (auto &kv : g_pectx) {
         PeCtx *x = kv.second;
         if (x->dscratch) (void) hipFree(x->dscratch);
@@ -667,6 +819,13 @@ int osgpu_set_path(int path)
     if (path < OSGPU_PATH_AUTO || path > OSGPU_PATH_PULL) return OSGPU_EINVAL;
     std::lock_guard<std::mutex> lk(g_mu);
     g_path = path;
+    return OSGPU_OK;
+}
+
+int osgpu_set_fused_max_bytes(long long bytes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_fused_max = bytes < 0 ? -1 : bytes;
     return OSGPU_OK;
 }
 

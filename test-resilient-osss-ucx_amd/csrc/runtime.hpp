@@ -45,7 +45,10 @@ int debug_level();
 // ----------------------------------------------------------- synchronisation
 
 int env_choice(const char *var, const char *alt, int def_is_alt);
-void entry_sync(const char *where);
+enum { ENTRY_DEVICE = 0, ENTRY_SPIN, ENTRY_STREAM, ENTRY_NONE };
+int entry_mode();
+void entry_sync(const char *where, hipStream_t own = nullptr);
+void entry_order(const char *where, hipStream_t st);
 void stream_wait(const char *where, hipStream_t st);
 
 // --------------------------------------------------------------- type info
@@ -139,6 +142,37 @@ struct StageSet {
     char *region(int i) const { return peer[i]; }  // the whole 4-slot area
 };
 StageSet *stage_setup(const Coll &c);
+
+// Publish a device allocation to every member of the active set and map
+// every member's (collective; the same verdict on every member).
+// distinct_processes: fail unless every member is its own process.
+// max_share: the largest number of members on one GPU.
+bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &peer,
+                 std::vector<void *> &opened, int *ndev, bool distinct_processes,
+                 int *max_share);
+
+// ------------------------------------------------- device-side barriers
+
+// Flag areas of one PE for one active set (fused.hip protocol): mine and
+// every member's, mapped.  `epoch` counts the fused calls made on the set.
+struct SyncSet {
+    bool ok = false;
+    int idx = -1;                              // my active-set index
+    unsigned long long *local = nullptr;       // my flag area (uncached HBM)
+    std::vector<unsigned long long *> peer;    // by active-set index
+    std::vector<void *> opened;                // IPC mappings to close
+    unsigned long long epoch = 0;
+    unsigned long long timeout = 0;            // wall-clock ticks
+    double timeout_s = 0;
+    int max_blocks = 0;                        // workgroups per fused launch
+    int *err_h = nullptr, *err_d = nullptr;    // host-mapped error word
+    unsigned long long *done_h = nullptr, *done_d = nullptr;  // host-mapped completion epoch
+};
+SyncSet *sync_setup(const Coll &c);
+
+// Per-PE byte limit of the fused path: osgpu_set_fused_max_bytes, else
+// OSGPU_FUSED_MAX_BYTES, else 1 MiB; 0 = fused path off.
+size_t fused_max_bytes();
 
 }  // namespace rt
 }  // namespace osgpu

@@ -39,6 +39,8 @@ namespace {
 
 using namespace osgpu::rt;
 
+thread_local int t_last_path = OSGPU_RAN_NONE;
+
 // ------------------------------------------------------------- the paths
 
 // one reduce-to-all call: the active set (Coll) plus the arrays
@@ -61,6 +63,21 @@ bool p2p_sources(const Call &c, std::vector<const void *> &srcs)
         char *p = nullptr;
         if (!heap_peer(order[k], seg, off, c.nbytes, &p)) return false;
         srcs[k] = p;
+    }
+    return true;
+}
+
+// every member's source in active-set order (the fused pull form)
+bool member_sources(const Call &c, std::vector<const void *> &srcs)
+{
+    int seg = -1;
+    size_t off = 0;
+    if (!heap_locate(c.me, c.source, c.nbytes, &seg, &off)) return false;
+    srcs.resize(c.PE_size);
+    for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
+        char *p = nullptr;
+        if (!heap_peer(pe, seg, off, c.nbytes, &p)) return false;
+        srcs[i] = p;
     }
     return true;
 }
@@ -104,9 +121,10 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
         sp[i] = (const char *) srcs[i] + (size_t) lo * s;
         dp[i] = (char *) dsts[i] + (size_t) lo * s;
     }
+    t_last_path = OSGPU_RAN_TEAM;
     DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
         c.nreduce, c.PE_size);
-    entry_sync(c.name);
+    entry_sync(c.name, st);
     barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
     if (hi > lo) {
         hipError_t e = osgpu::launch_team(c.type, c.op, c.PE_size, dp.data(), sp.data(),
@@ -122,8 +140,9 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
 void run_p2p(const Call &c, const std::vector<const void *> &srcs)
 {
     hipStream_t st = pe_stream(c.name, c.me);
+    t_last_path = OSGPU_RAN_PULL;
     // prior device work of this process that produced `source` must be done
-    entry_sync(c.name);
+    entry_sync(c.name, st);
     barrier(c);  // src/reductions.c:82 -- every source is ready
     const bool overlap = c.PE_size > 1 && ranges_overlap(c.target, c.source, c.nbytes);
     void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
@@ -136,6 +155,126 @@ void run_p2p(const Call &c, const std::vector<const void *> &srcs)
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
         stream_wait(c.name, st);
     }
+}
+
+// ---------------------------------------------------- fused small calls
+
+// A device-resident call of at most fused_max_bytes() per PE runs as ONE
+// launch with its barriers on the device (fused.hip); larger calls keep the
+// host barriers around the full-chip streaming kernels.
+// Only with entry ordering that does not wait for this PE's own stream:
+// under hipDeviceSynchronize every call would first wait for the previous
+// fused launch to retire (measured 26 us per 1 Ki-int call against 16 us on
+// the host-barrier path; 12 us with `stream` ordering).
+// The pull form reads P sources per PE (P times the team form's bytes) on
+// its share of the CUs: its limit is a quarter of the team form's (measured
+// with 4 processes on one GPU at 1 MiB per PE: fused pull 42 us against 29
+// us with host barriers; fused team 23 us).
+bool fused_eligible(const Call &c, bool team)
+{
+    const int em = entry_mode();
+    const size_t lim = team ? fused_max_bytes() : fused_max_bytes() / 4;
+    return (em == ENTRY_STREAM || em == ENTRY_NONE) && osgpu::fused_supported(c.type) &&
+           c.PE_size >= 2 && c.PE_size <= osgpu::kMaxTeam && c.nbytes <= lim &&
+           c.ops.getmem != nullptr;
+}
+
+// Completion of a fused call: spin on the host-mapped word the kernel's
+// last workgroup writes once every member is done (no wait for the launch to
+// retire); the stream is polled now and then so a launch that ended without
+// writing it (a timed-out barrier) is noticed.
+void fused_wait(const Call &c, const SyncSet &S, hipStream_t st, unsigned long long epoch)
+{
+    for (unsigned it = 1;; it++) {
+        if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
+        if (__atomic_load_n(S.err_h, __ATOMIC_RELAXED)) return;  // reported by the caller
+        if ((it & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
+                return;  // ended without completing: the error word says why
+            }
+            if (q != hipErrorNotReady) fatal(c.name, "fused launch: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// team = true: owner-computes over every member's target (srcs/dsts in
+// active-set order); false: pull form, my own target from every source.
+void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
+               const std::vector<void *> &dsts, bool team)
+{
+    hipStream_t st = pe_stream(c.name, c.me);
+    const size_t s = type_size(c.type);
+    const int P = c.PE_size, idx = S.idx;
+    osgpu::FusedArgs a;
+    memset(&a, 0, sizeof(a));
+    long long lo = 0, hi = c.nreduce;
+    if (team) osgpu_shard_range(c.nreduce, P, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
+    const bool overlap = !team && ranges_overlap(c.target, c.source, c.nbytes);
+    void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
+    for (int i = 0; i < P; i++) {
+        a.src[i] = (const char *) srcs[i] + (size_t) lo * s;
+        a.flags[i] = S.peer[i];
+    }
+    if (team) {
+        for (int d = 0; d < P; d++) {
+            a.dst[d] = (char *) dsts[d] + (size_t) lo * s;
+            a.q[d] = d;
+        }
+        a.D = P;
+    } else {
+        a.dst[0] = out;
+        a.q[0] = idx;
+        a.D = 1;
+    }
+    a.mine = S.local;
+    a.err = S.err_d;
+    a.done_host = S.done_d;
+    a.epoch = ++S.epoch;
+    a.timeout = S.timeout;
+    a.n = (size_t) (hi - lo);
+    a.P = P;
+    a.me = idx;
+    a.max_blocks = S.max_blocks;
+    t_last_path = team ? OSGPU_RAN_FUSED_TEAM : OSGPU_RAN_FUSED_PULL;
+    DBG("%s PE %d: fused %s path, epoch %llu, [%lld, %lld)", c.name, c.me,
+        team ? "team" : "pull", a.epoch, lo, hi);
+    // OSGPU_FUSED_TRACE=1: phase clocks of workgroup 0 / the last workgroup
+    static unsigned long long *trace = [] {
+        unsigned long long *p = nullptr;
+        if (getenv("OSGPU_FUSED_TRACE") &&
+            hipHostMalloc((void **) &p, 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess)
+            p = nullptr;
+        return p;
+    }();
+    a.trace = trace;
+    entry_order(c.name, st);
+    hipError_t e = osgpu::launch_fused(c.type, c.op, a, st);
+    if (e != hipSuccess) fatal(c.name, "fused launch: %s", hipGetErrorString(e));
+    if (overlap) {
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
+        stream_wait(c.name, st);
+    } else {
+        fused_wait(c, S, st, a.epoch);
+    }
+    if (trace) {
+        const double tk = 1e6 / 1e8;  // us per tick of the 100 MHz wall clock
+        fprintf(stderr, "[osgpu fused PE %d epoch %llu] arrive-wait %.2f body %.2f fence %.2f "
+                        "ticket+fence %.2f done-wait %.2f us\n", c.me, a.epoch,
+                (trace[1] - trace[0]) * tk, (trace[2] - trace[1]) * tk,
+                (trace[3] - trace[2]) * tk, (trace[4] - trace[3]) * tk,
+                (trace[6] - trace[5]) * tk);
+    }
+    const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
+    if (!err && !overlap && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < a.epoch)
+        fatal(c.name, "fused launch ended without completing epoch %llu", a.epoch);
+    if (err)
+        fatal(c.name, "device barrier (%s) timed out after %.1f s: a member of the active "
+                      "set did not enter or finish the call",
+              err == 1 ? "entry" : "exit", S.timeout_s);
 }
 
 bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *mult)
@@ -177,6 +316,7 @@ void run_rccl(const Call &c)
     ncclRedOp_t rop;
     size_t mult;
     rccl_types(c.type, c.op, &dt, &rop, &mult);
+    t_last_path = OSGPU_RAN_RCCL;
     hipStream_t st = pe_stream(c.name, c.me);
     entry_sync(c.name);
     const bool overlap = ranges_overlap(c.target, c.source, c.nbytes) && c.target != c.source;
@@ -197,6 +337,7 @@ void run_staged(const Call &c, StageSet &S)
     const size_t C = S.slot / s;                       // elements per chunk
     const size_t N = (size_t) c.nreduce;
     const size_t nchunks = (N + C - 1) / C;
+    t_last_path = OSGPU_RAN_STAGED;
     const int P = c.PE_size;
     int idx = 0;
     for (int i = 0, pe = c.PE_start; i < P; i++, pe += c.step)
@@ -280,6 +421,7 @@ void run_host(const Call &c)
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
     const int P = c.PE_size;
+    t_last_path = OSGPU_RAN_GETMEM;
     std::vector<int> order(P);
     fold_order(c.me, c.PE_start, c.step, P, order.data());
 
@@ -335,6 +477,7 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     c.source = source;
     c.nreduce = nreduce;
     if (nreduce <= 0) {  // nothing to combine; the collective still syncs
+        t_last_path = OSGPU_RAN_BARRIER_ONLY;
         barrier(c);
         barrier(c);
         return;
@@ -364,11 +507,20 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     std::vector<const void *> srcs;
     std::vector<void *> dsts;
     int idx = -1;
+    SyncSet *S = nullptr;
     if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_P2P) &&
         (idx = team_ptrs(c, srcs, dsts)) >= 0) {
-        run_team(c, srcs, dsts, idx);
-    } else if (mode != OSGPU_PATH_RCCL && p2p_sources(c, srcs)) {
-        run_p2p(c, srcs);
+        if (fused_eligible(c, true) && (S = sync_setup(c)))
+            run_fused(c, *S, srcs, dsts, true);
+        else
+            run_team(c, srcs, dsts, idx);
+    } else if (mode != OSGPU_PATH_RCCL && member_sources(c, srcs)) {
+        if (fused_eligible(c, false) && (S = sync_setup(c))) {
+            run_fused(c, *S, srcs, dsts, false);
+        } else {
+            p2p_sources(c, srcs);
+            run_p2p(c, srcs);
+        }
     } else if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_RCCL) && rccl_usable(c)) {
         run_rccl(c);
     } else {
@@ -382,6 +534,8 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
 }
 
 }  // namespace
+
+extern "C" int osgpu_last_path(void) { return t_last_path; }
 
 // ======================================================================
 // Part 1: the 44 entry points (pshmem_* strong, shmem_* weak aliases, as in

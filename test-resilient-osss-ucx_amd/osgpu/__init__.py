@@ -30,6 +30,9 @@ CTYPE = {
     "complexf": ctypes.c_float * 2, "complexd": ctypes.c_double * 2,
 }
 PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
+# enum osgpu_ran: what osgpu_last_path() reports
+RAN = ["none", "team", "pull", "rccl", "staged", "getmem", "fused_team", "fused_pull",
+       "barrier_only"]
 
 
 def has_op(t: str, op: str) -> bool:
@@ -130,10 +133,17 @@ def load() -> ctypes.CDLL:
                                     ctypes.POINTER(ctypes.c_longlong)]
     L.osgpu_host_register.argtypes = [vp, sz]
     L.osgpu_host_unregister.argtypes = [vp]
+    L.osgpu_set_fused_max_bytes.argtypes = [ctypes.c_longlong]
+    L.osgpu_last_path.restype = ctypes.c_int
     L.osgpu_last_error.restype = ctypes.c_char_p
     L.osgpu_version.restype = ctypes.c_char_p
     _LIB = L
     return L
+
+
+def last_path() -> str:
+    """Name of the path the calling thread's last reduce-to-all call took."""
+    return RAN[load().osgpu_last_path()]
 
 
 def to_all(t: str, op: str):

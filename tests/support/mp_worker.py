@@ -16,6 +16,14 @@ modes
         parent to check
   hoststaged  GPU, host heaps in shared memory: reductions and collectives
         on the STAGED and GETMEM paths
+  golden  GPU, IPC device heaps + shared-memory runtime: every golden case
+        whose PEs fit in the job (tests/golden/reduce_cases.json), team and
+        pull form, so small calls run the fused one-launch path with its
+        device-side barriers between processes; per-PE SHA-256 and the path
+        taken are written for the parent; then calls around a 64 KiB fused
+        limit are checked against the oracle
+  latency  GPU, same setup: per-call time of shmem_int_sum_to_all, fused
+        path vs host barriers (bench/tool use)
 usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. \
        python mp_worker.py MODE OUTDIR
 """
@@ -76,6 +84,147 @@ def run_colls(L, rank, world, src_addr, tgt_addr, psync, out, tag, write, read):
         dist.barrier()
 
 
+def device_heap_modes(L, PES, mode, rank, world):
+    import time
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    H = 40 << 20
+    heap = torch.zeros(H, dtype=torch.uint8, device="cuda:0")
+    h = (ctypes.c_char * 64)()
+    assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
+    hs = [None] * world
+    dist.all_gather_object(hs, bytes(h))
+    mapped = []
+    for pe in range(world):
+        base = heap.data_ptr()
+        if pe != rank:
+            base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(hs[pe]))
+            assert base, L.osgpu_last_error().decode()
+            mapped.append(base)
+        assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), H) == 0
+    psync = PES.pes_heap(rank) + (1 << 24) - 8192
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    sync = lambda: PES.pes_barrier(0, 0, world, None)  # noqa: E731
+    wrk = (ctypes.c_byte * 4096)()
+    dev0 = heap.data_ptr()
+    res = {}
+
+    def put(off, arr):
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        if raw.size:
+            heap[off:off + raw.size].copy_(torch.from_numpy(raw.copy()).cuda())
+
+    if mode == "golden":
+        digests, paths = {}, {}
+        for ci, c in enumerate(O.load_cases()):
+            if c["npes"] > world:
+                continue
+            t, op, n = c["type"], c["op"], c["nreduce"]
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            act = O.active_set(c["PE_start"], c["logPE_stride"], c["PE_size"])
+            toff = max(4096, (n * s + 4095) // 4096 * 4096)
+            if rank < c["npes"]:
+                put(0, O.case_inputs(c)[rank])
+            fn = getattr(L, f"shmem_{t}_{op}_to_all")
+            for path in (osgpu.PATH_AUTO, osgpu.PATH_PULL):
+                L.osgpu_set_path(path)
+                heap[toff:toff + max(n * s, 16)].fill_(0xA5)
+                torch.cuda.synchronize()
+                sync()
+                if rank in act:
+                    fn(dev0 + toff, dev0, n, c["PE_start"], c["logPE_stride"], c["PE_size"],
+                       wrk, psync)
+                    paths[f"{ci}/{path}"] = osgpu.last_path()
+                    got = heap[toff:toff + n * s].cpu().numpy()
+                    if t == "longdouble":
+                        got = got.reshape(-1, 16)[:, :10].reshape(-1)
+                    digests[f"{ci}/{path}"] = O.digest(O.from_value_bytes(t, got))
+                    assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
+                sync()
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        res["digests"], res["paths"] = digests, paths
+        # around a 64 KiB fused limit: under, at, just over
+        lim = 64 << 10
+        L.osgpu_set_fused_max_bytes(lim)
+        bound = {}
+        for t, op in (("double", "sum"), ("float", "prod"), ("int", "sum")):
+            s = np.dtype(O.NP_DTYPE[t]).itemsize
+            for n in (lim // s - 5, lim // s, lim // s + 1, lim // 4 // s, lim // 4 // s + 1):
+                src = O.team_inputs(t, world, n, 0x77 + n, "wide")
+                want = O.to_all(t, op, src)[rank]
+                toff = (n * s + 4095) // 4096 * 4096
+                for path in (osgpu.PATH_AUTO, osgpu.PATH_PULL):
+                    L.osgpu_set_path(path)
+                    put(0, src[rank])
+                    heap[toff:toff + n * s].fill_(0x5A)
+                    torch.cuda.synchronize()
+                    sync()
+                    getattr(L, f"shmem_{t}_{op}_to_all")(dev0 + toff, dev0, n, 0, 0, world,
+                                                         wrk, psync)
+                    got = heap[toff:toff + n * s].cpu().numpy()
+                    bound[f"{t}/{op}/{n}/{path}"] = [
+                        bool(np.array_equal(got, want.view(np.uint8).reshape(-1))),
+                        osgpu.last_path(),
+                        n * s <= (lim if path == osgpu.PATH_AUTO else lim // 4)]
+                    sync()
+        L.osgpu_set_fused_max_bytes(-1)
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        res["boundary"] = bound
+    else:  # latency
+        reps = int(os.environ.get("MP_REPS", "300"))
+        lat = {}
+        for n in [int(x) for x in os.environ.get("MP_SIZES", "1024,65536,1048576").split(",")]:
+            put(0, np.arange(n, dtype=np.int32) + rank)
+            toff = (n * 4 + 4095) // 4096 * 4096
+            torch.cuda.synchronize()
+            for name, path, lim in (("team", osgpu.PATH_AUTO, 0), ("pull", osgpu.PATH_PULL, 0),
+                                    ("fused_team", osgpu.PATH_AUTO, 1 << 30),
+                                    ("fused_pull", osgpu.PATH_PULL, 1 << 30)):
+                L.osgpu_set_path(path)
+                L.osgpu_set_fused_max_bytes(lim)
+                ts, evs = [], []
+                events = os.environ.get("MP_EVENTS") == "1"  # GPU-side span (own stream)
+                if events:
+                    st = torch.cuda.Stream()
+                    L.osgpu_set_stream(ctypes.c_void_p(st.cuda_stream))
+                for r in range(reps + 5):
+                    if events:
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                    sync()
+                    t0 = time.perf_counter()
+                    if events:
+                        e0.record(st)
+                    L.shmem_int_sum_to_all(dev0 + toff, dev0, n, 0, 0, world, wrk, psync)
+                    if events:
+                        e1.record(st)
+                    sync()
+                    ts.append(time.perf_counter() - t0)
+                    if events:
+                        evs.append((e0, e1))
+                torch.cuda.synchronize()
+                gpu = [a.elapsed_time(b) * 1e3 for a, b in evs[5:]] or [float("nan")]
+                if events:
+                    L.osgpu_set_stream(None)
+                ran = osgpu.last_path()
+                got = heap[toff:toff + n * 4].view(torch.int32).cpu().numpy()
+                ok = bool(np.array_equal(got, world * np.arange(n, dtype=np.int32)
+                                         + world * (world - 1) // 2))
+                lat[f"{n}/{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
+                                      "gpu_us_median": float(np.median(gpu)),
+                                      "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
+                                      "path": ran, "correct": ok}
+        L.osgpu_set_fused_max_bytes(-1)
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        res["latency"] = lat
+    dist.barrier()
+    L.osgpu_finalize()
+    for p in mapped:
+        L.osgpu_ipc_close(ctypes.c_void_p(p))
+    return res
+
+
 def main():
     mode, outdir = sys.argv[1], sys.argv[2]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -83,7 +232,8 @@ def main():
     L = osgpu.load()
     counter = [0]
     PES = None
-    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in ("hoststaged", "hostcoll"):
+    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in ("hoststaged", "hostcoll",
+                                                                     "golden", "latency"):
         from support import peshm
         PES = peshm.init(rank, world, 1 << 24, dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -124,6 +274,8 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
+    if mode in ("golden", "latency"):
+        res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096
         buf = PES.pes_heap(rank)
@@ -172,24 +324,33 @@ def main():
             src = O.gen_input(t, n, O.pe_seed(0xABC, rank), dist_)
             toff = (n * s + 4095) // 4096 * 4096
             raw = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
-            for path, inplace in ((osgpu.PATH_AUTO, False), (osgpu.PATH_PULL, False),
-                                  (osgpu.PATH_AUTO, True)):
+            # fused: -1 = default (one launch, device barriers, when the
+            # runtime has getmem for the flag-area exchange), 0 = host barriers
+            for path, inplace, fused in ((osgpu.PATH_AUTO, False, -1), (osgpu.PATH_AUTO, False, 0),
+                                         (osgpu.PATH_PULL, False, -1), (osgpu.PATH_PULL, False, 0),
+                                         (osgpu.PATH_AUTO, True, -1)):
                 heap[: raw.size].copy_(torch.from_numpy(raw.copy()).cuda())
                 torch.cuda.synchronize()
                 L.osgpu_set_path(path)
-                psync = (ctypes.c_long * 128)()
+                L.osgpu_set_fused_max_bytes(fused)
+                # pSync must be symmetric (getmem-able) when the runtime has getmem
+                psync = (PES.pes_heap(rank) + (1 << 24) - 8192 if PES is not None
+                         else ctypes.addressof((ctypes.c_long * 128)()))
                 wrk = (ctypes.c_byte * 4096)()
                 tgt = heap.data_ptr() + (0 if inplace else toff)
                 dist.barrier()
                 getattr(L, f"shmem_{t}_{op}_to_all")(tgt, heap.data_ptr(), n, 0, 0, world,
                                                      wrk, psync)
+                ran = osgpu.last_path()
                 torch.cuda.synchronize()
                 got = heap[(0 if inplace else toff):(0 if inplace else toff) + n * s].cpu().numpy()
                 if t == "longdouble":
                     got = got.reshape(-1, 16)[:, :10].reshape(-1)
-                out[f"{t}/{op}/{path}/{int(inplace)}"] = got.tobytes().hex()
+                out[f"{t}/{op}/{path}/{int(inplace)}/{fused}"] = got.tobytes().hex()
+                res.setdefault("paths", {})[f"{t}/{op}/{path}/{int(inplace)}/{fused}"] = ran
                 dist.barrier()
         L.osgpu_set_path(osgpu.PATH_AUTO)
+        L.osgpu_set_fused_max_bytes(-1)
         if PES is not None:  # collect needs the runtime's getmem (pSync words)
             psync = PES.pes_heap(rank) + (1 << 24) - 4096
 

@@ -60,31 +60,37 @@ class Team:
         self.H = _align(heap_bytes) + 4096
         self.psync_off = self.H - 4096
         self.device = device
-        assert self.pet.pet_init(npes) == 0
-        assert self.lib.osgpu_set_pe_ops(self.pet.pet_ops()) == 0
-        for pe in range(64):
-            self.lib.osgpu_heap_unregister(pe)
         if device:
             import torch
             self.torch = torch
             self.buf = torch.zeros(npes * self.H, dtype=torch.uint8, device="cuda:0")
             self.base = self.buf.data_ptr()
-            for pe in range(npes):
-                assert self.lib.osgpu_heap_register(pe, self.base + pe * self.H, self.H) == 0
             # pSync is host memory in every OpenSHMEM program: a small host
             # symmetric heap per PE holds it (getmem-able, like the UCX heap)
             self.pbuf = np.zeros(npes * 4096 + 256, dtype=np.uint8)
             a = self.pbuf.ctypes.data
             self.poff = (-a) % 256
             self.pbase = a + self.poff
-            for pe in range(npes):
-                assert self.pet.pet_register_host_heap(pe, self.pbase + pe * 4096, 4096) == 0
         else:
             self.hbuf = np.zeros(npes * self.H + 256, dtype=np.uint8)
             a = self.hbuf.ctypes.data
             self.hoff = (-a) % 256
             self.base = a + self.hoff
-            for pe in range(npes):
+        self.activate()
+
+    def activate(self):
+        """Make this team the one the PE-thread runtime and the library serve
+        (another Team may have re-initialised them since): PE services,
+        device heaps, host heaps (the pSync heap of a device team)."""
+        assert self.pet.pet_init(self.npes) == 0
+        assert self.lib.osgpu_set_pe_ops(self.pet.pet_ops()) == 0
+        for pe in range(64):
+            self.lib.osgpu_heap_unregister(pe)
+        for pe in range(self.npes):
+            if self.device:
+                assert self.lib.osgpu_heap_register(pe, self.base + pe * self.H, self.H) == 0
+                assert self.pet.pet_register_host_heap(pe, self.pbase + pe * 4096, 4096) == 0
+            else:
                 assert self.pet.pet_register_host_heap(pe, self.base + pe * self.H, self.H) == 0
 
     def ptr(self, pe: int, off: int) -> int:
@@ -147,11 +153,13 @@ class Team:
         """Run call(pe) on one thread per member PE (a blocking collective),
         then check every member's pSync is back at SHMEM_SYNC_VALUE."""
         errs = []
+        self.last_paths = {}
 
         def body(pe):
             try:
                 self.pet.pet_set_me(pe)
                 call(pe)
+                self.last_paths[pe] = self.osgpu.last_path()
             except Exception as e:  # pragma: no cover
                 errs.append(e)
 

@@ -42,14 +42,7 @@ def team(device=True):
     if key not in _TEAMS:
         _TEAMS[key] = T.Team(8, 20 << 20, device=device)
     tm = _TEAMS[key]
-    tm.pet.pet_init(8)
-    tm.lib.osgpu_set_pe_ops(tm.pet.pet_ops())
-    if device:
-        for pe in range(8):
-            tm.lib.osgpu_heap_register(pe, tm.base + pe * tm.H, tm.H)
-    else:
-        for pe in range(8):
-            tm.pet.pet_register_host_heap(pe, tm.base + pe * tm.H, tm.H)
+    tm.activate()
     return tm
 
 
@@ -95,11 +88,23 @@ def _by_pair():
     return sorted(pairs.items())
 
 
+def _expected_path(c, team_form):
+    """Path the library must have taken.  PEs here are threads of one
+    process: the fused one-launch path needs every member in its own process
+    (tests/test_multiproc.py covers it), so these calls keep host barriers."""
+    if c["nreduce"] == 0:
+        return "barrier_only"
+    return "team" if team_form and c["PE_size"] >= 2 else "pull"
+
+
 @pytest.mark.parametrize("pair,cases", _by_pair(), ids=lambda x: "%s" % (x,) if isinstance(x, tuple) else "")
 def test_device_resident_matches_golden(torch_cuda, pair, cases):
     tm = team(device=True)
     for c in cases:
         check(c, run_case(tm, c))
+        act = O.active_set(c["PE_start"], c["logPE_stride"], c["PE_size"])
+        want = _expected_path(c, True)
+        assert all(tm.last_paths[pe] == want for pe in act), (tm.last_paths, want)
 
 
 def test_pull_path_matches_golden(torch_cuda):
@@ -111,6 +116,7 @@ def test_pull_path_matches_golden(torch_cuda):
         for c in CASES:
             if c["nreduce"] <= 4097 and c["npes"] in (2, 3, 8) and c["tag"] != "subset":
                 check(c, run_case(tm, c))
+                assert tm.last_paths[c["PE_start"]] == _expected_path(c, False)
     finally:
         tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
 

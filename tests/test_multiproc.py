@@ -109,6 +109,22 @@ def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
              ("int", "prod", 1000, "bits"), ("complexd", "prod", 999, "edge"),
              ("longdouble", "sum", 517, "wide"), ("short", "xor", 4096, "bits"))
     _check_specs(res, specs, 0xABC)
+    # which path ran: with the shm runtime (getmem available) calls of at most
+    # 1 MiB per PE (team form; 256 KiB pull form) take the fused one-launch
+    # path unless it is switched off (suffix /0); long double and the gloo
+    # runtime keep host barriers
+    for t, op, n, _ in specs:
+        for r in range(2):
+            for key, ran in res[r]["paths"].items():
+                if not key.startswith(f"{t}/{op}/"):
+                    continue
+                path, inplace, fused = key.split("/")[2:]
+                team = path == "0" and inplace == "0"
+                s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+                fusable = (pes == "shm" and fused == "-1" and t != "longdouble" and
+                           n * s <= (1 << 20) // (1 if team else 4))
+                want = ("fused_" if fusable else "") + ("team" if team else "pull")
+                assert ran == want, (key, r, ran)
     if pes == "shm":  # collect needs getmem: the shm runtime has it
         _check_colls(res, "device")
 
@@ -132,3 +148,43 @@ def test_host_staged_processes(tmp_path, world, monkeypatch):
     _check_colls(res, "staged")
     _check_colls(res, "getmem")
 
+
+
+@pytest.mark.gpu
+def test_fused_path_golden_processes(tmp_path):
+    """Four processes share cuda:0 (IPC device heaps, shared-memory runtime):
+    every golden case with at most 4 PEs, team and pull form.  Calls of at
+    most 1 MiB per PE (all types but long double) run as ONE launch whose
+    barriers are device flags written across processes; the rest keep host
+    barriers.  Per-PE results bit-exact against the reference digests, and
+    calls around a 64 KiB fused limit bit-exact against the oracle."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 4
+    res = launch("golden", world, tmp_path)
+    cases = O.load_cases()
+    nfused = nchecked = 0
+    for r in range(world):
+        for key, dg in res[r]["digests"].items():
+            ci, path = key.split("/")
+            c = cases[int(ci)]
+            assert dg == c["digests"][str(r)], (c["type"], c["op"], c["npes"], c["nreduce"],
+                                                c["tag"], path, r)
+            nchecked += 1
+            s = 16 if c["type"] == "longdouble" else np.dtype(O.NP_DTYPE[c["type"]]).itemsize
+            ran = res[r]["paths"][key]
+            if c["nreduce"] == 0:
+                want = "barrier_only"
+            else:
+                team = path == "0" and c["PE_size"] >= 2
+                fused = (c["type"] != "longdouble" and c["PE_size"] >= 2 and
+                         c["nreduce"] * s <= (1 << 20) // (1 if team else 4))
+                want = ("fused_" if fused else "") + ("team" if team else "pull")
+            assert ran == want, (key, r, ran, want)
+            nfused += ran.startswith("fused_")
+    assert nchecked > 2000 and nfused > 1500, (nchecked, nfused)
+    for r in range(world):
+        for key, (exact, ran, fused) in res[r]["boundary"].items():
+            assert exact, (key, r)
+            assert ran.startswith("fused_") == fused, (key, r, ran)

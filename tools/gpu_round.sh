@@ -22,6 +22,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
     tune)  step tune 300 ./tools/tune_combine ;;
+    latency) step latency 300 python tools/latency_probe.py ;;
+    mplat) step mplat 400 python tools/mp_latency.py ;;
     multi) step multi2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --nreduce $((64<<20)) --c4-nreduce $((256<<20)) --c5-nreduce $((64<<20)) --deadline 200 ;;
     multi_s) step multi2 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 120 ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&

@@ -35,15 +35,21 @@ for n in SIZES:
         tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
         src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
         if device:
-            paths = (("team", osgpu.PATH_AUTO), ("pull", osgpu.PATH_PULL))
+            # host barriers (fused off) vs one launch with device barriers
+            paths = (("team", osgpu.PATH_AUTO, 0), ("pull", osgpu.PATH_PULL, 0),
+                     ("fused_team", osgpu.PATH_AUTO, 1 << 30),
+                     ("fused_pull", osgpu.PATH_PULL, 1 << 30))
             sel = os.environ.get("PROBE_PATHS")
             if sel:
                 paths = [p for p in paths if p[0] in sel.split(",")]
-            for name, path in paths:
+            ps = (ctypes.c_void_p * 2)(tm.psync_ptr(0), tm.psync_ptr(1))
+            for name, path, lim in paths:
                 tm.lib.osgpu_set_path(path)
+                tm.lib.osgpu_set_fused_max_bytes(lim)
                 row[name + "_us"] = tm.pet.pet_time_to_all(
-                    fn, 2, tgt, src, None, n, int(os.environ.get("PROBE_REPS", "200"))) * 1e6
+                    fn, 2, tgt, src, ps, n, int(os.environ.get("PROBE_REPS", "200"))) * 1e6
             tm.lib.osgpu_set_path(osgpu.PATH_AUTO)
+            tm.lib.osgpu_set_fused_max_bytes(-1)
         else:
             ps = (ctypes.c_void_p * 2)(tm.ptr(0, tm.psync_off), tm.ptr(1, tm.psync_off))
             row["host_staged_us"] = tm.pet.pet_time_to_all(fn, 2, tgt, src, ps, n, 200) * 1e6
