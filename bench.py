@@ -13,7 +13,9 @@ N = 1 (default) -- BASELINE config 2: nreduce = 64 Mi doubles, 1 MI355X,
   Extra fields: roofline (HIP events on the launch stream + PMC traffic from
   profiles/), the full C-API call (2 PEs, timed in C), the host-staged
   (PCIe-inclusive) rate, the data-movement collectives (copy kernel roofline,
-  fcollect64 through the C ABI), the reference's CPU loop shape on this host.
+  fcollect64 through the C ABI), BASELINE config 1's small call (1 Ki ints,
+  2 PE processes: fused one-launch path vs host barriers vs the reference's
+  loop on 2 cores), the reference's CPU loop shape on this host.
 
 N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   shmem_double_sum_to_all(nreduce = 64 Mi per PE) over all N PEs (weak
@@ -197,6 +199,34 @@ def api_call_time(n, reps=20):
     return out
 
 
+def small_call_latency(n=1024, reps=300):
+    """BASELINE config 1's shape (shmem_int_sum_to_all, nreduce = 1 Ki, 2 PEs)
+    with one PROCESS per PE, both on this GPU (IPC device heaps, the
+    shared-memory PE runtime of tests/support/pe_shm.c): median per call of
+    the fused one-launch path (device-side barriers) and of the host-barrier
+    path, timed barrier to barrier (tools/mp_latency.py), next to the
+    reference's loop shape on 2 host cores."""
+    import subprocess
+    import oracle as O
+    env = dict(os.environ, MP_WORLDS="2", MP_SIZES=str(n), MP_REPS=str(reps))
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mp_latency.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-400:]}
+    lat = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["latency"]
+    out = {"note": f"shmem_int_sum_to_all nreduce={n}, 2 PEs = 2 processes sharing this GPU, "
+                   f"device-resident symmetric heaps, median of {reps} calls barrier to barrier"}
+    for k in ("fused_team", "team"):
+        v = lat[f"{n}/{k}"]
+        out[k + "_us"] = v["us_median"]
+        out[k + "_correct"] = v["correct"]
+    src = O.team_inputs("int", 2, n, 5, "bits")
+    out["cpu_reference_loop_us"] = O.cpu_baseline("int", "sum", src, reps=2000, pin=True) * 1e6
+    return out
+
+
 def bench_single(args):
     import torch
     import osgpu
@@ -277,6 +307,10 @@ def bench_single(args):
             res["collectives"] = collectives_single()
         except Exception as e:
             res["collectives"] = {"error": repr(e)}
+        try:
+            res["small_call"] = small_call_latency()
+        except Exception as e:
+            res["small_call"] = {"error": repr(e)}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_n)
     print(json.dumps(res), flush=True)

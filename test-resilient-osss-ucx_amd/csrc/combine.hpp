@@ -57,7 +57,9 @@ hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
 // flag area (unsigned long long):
 constexpr int kFlagArrive = 0;    // [0, 8): arrive[member]
 constexpr int kFlagDone = 8;      // [8, 16): done[member]
-constexpr int kFlagTicket = 16;   // last-workgroup ticket (u32)
+constexpr int kFlagTicket = 16;   // last-workgroup tickets (u32): completion,
+constexpr int kFlagTicketIn = 17;  //   staged copy-in,
+constexpr int kFlagTicketOut = 18; //   staged copy-out
 constexpr int kFlagWords = 32;
 // fused grids: at most one workgroup of 256 lanes per CU of the GPU (256 on
 // MI355X), split between the members sharing it (one member per GPU: all)
@@ -76,6 +78,12 @@ struct FusedArgs {
     int nedge, P, D, me;                  // me: my active-set index
     int max_blocks;                       // grid cap (co-residency on a shared GPU)
     unsigned long long *trace;            // optional host-mapped phase clock (8 words)
+    // staged form (host memory): null host_in = device form
+    const void *host_in;                  // my host source (device-accessible)
+    void *host_out;                       // my host target (device-accessible)
+    void *stage_mine;                     // my input staging slot (= src[me])
+    const void *stage_result;             // my result staging slot (= one of dst[])
+    size_t host_bytes;
 };
 bool fused_supported(int type);
 hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s);

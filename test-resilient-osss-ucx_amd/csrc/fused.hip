@@ -30,6 +30,12 @@
 //     calling thread spins on -- it returns without waiting for the launch
 //     to retire (the launch-to-completion notification is most of the
 //     latency of a small call).
+// Staged form (host symmetric heaps, the reference's placement): step 1 is
+// preceded by the whole grid copying my host source (pinned, mapped) into
+// my device staging slot, the body folds the members' staging slots into
+// their result slots, and after step 4 every workgroup waits for the done
+// flags and copies my result slot to my host target -- H2D, exchange and
+// D2H of the STAGED path in the same single launch.
 // Waits are bounded (wall clock); a timeout sets a host-mapped error word,
 // which the host turns into a fatal error, and the grid still drains.
 //
@@ -146,15 +152,65 @@ __device__ __forceinline__ void do_elem(const FusedArgs &a, size_t i)
         if (d < a.D) static_cast<T *>(a.dst[d])[i] = r[d];
 }
 
+// Lane 0 of every workgroup, after the workgroup's stores: release them
+// system-wide and take ticket `w`; true for the last workgroup of the grid
+// (which resets the ticket for the next launch and acquires).
+__device__ __forceinline__ bool last_workgroup(const FusedArgs &a, int w)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (gridDim.x == 1) return true;
+    unsigned *ticket = reinterpret_cast<unsigned *>(a.mine + w);
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (t != gridDim.x - 1) return false;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    return true;
+}
+
+// Grid-stride byte copy between host memory (pinned, mapped) and a device
+// staging slot: 16-B vectors when both ends allow it, else dwords, else bytes.
+__device__ void stage_copy(void *dst, const void *src, size_t nbytes)
+{
+    const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
+    const size_t stride = (size_t) gridDim.x * kFBlock;
+    const uintptr_t al = (uintptr_t) dst | (uintptr_t) src;
+    if ((al & 15) == 0) {
+        const size_t nv = nbytes / 16;
+        for (size_t j = tid; j < nv; j += stride)
+            static_cast<u32x4 *>(dst)[j] = static_cast<const u32x4 *>(src)[j];
+        for (size_t b = nv * 16 + tid; b < nbytes; b += stride)
+            static_cast<char *>(dst)[b] = static_cast<const char *>(src)[b];
+    } else if ((al & 3) == 0) {
+        const size_t nw = nbytes / 4;
+        for (size_t j = tid; j < nw; j += stride)
+            static_cast<unsigned *>(dst)[j] = static_cast<const unsigned *>(src)[j];
+        for (size_t b = nw * 4 + tid; b < nbytes; b += stride)
+            static_cast<char *>(dst)[b] = static_cast<const char *>(src)[b];
+    } else {
+        for (size_t b = tid; b < nbytes; b += stride)
+            static_cast<char *>(dst)[b] = static_cast<const char *>(src)[b];
+    }
+}
+
 template <typename T, int OP, bool VEC>
 __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
 {
     __shared__ int s_go;
     const bool tr = a.trace && blockIdx.x == 0 && threadIdx.x == 0;
     if (tr) a.trace[0] = (unsigned long long) wall_clock64();
-    // 1. arrive (src/reductions.c:82 -- my source is ready, my target free)
-    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
+    // 1. arrive (src/reductions.c:82 -- my source is ready, my target free).
+    // Staged form: my host source is first copied into my staging slot by
+    // the whole grid; the last workgroup to finish its part arrives.
+    if (a.host_in) {
+        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
+            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
+    } else if (blockIdx.x == 0 && (int) threadIdx.x < a.P) {
         st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
+    }
     // 2. wait for every member's arrival
     if (threadIdx.x == 0)
         s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
@@ -209,29 +265,33 @@ __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
     __syncthreads();
     if (tr) a.trace[2] = (unsigned long long) wall_clock64();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        s_go = 1;
-        if (gridDim.x > 1) {
-            unsigned *ticket = reinterpret_cast<unsigned *>(a.mine + kFlagTicket);
-            const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            s_go = t == gridDim.x - 1;
-            if (s_go) {
-                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            }
-        }
+        s_go = last_workgroup(a, kFlagTicket);
         if (tr) a.trace[3] = (unsigned long long) wall_clock64();
         if (s_go) {
             if (a.trace) a.trace[4] = a.trace[5] = (unsigned long long) wall_clock64();
             for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
-            if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2)) {
+            if (!a.host_out && wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2)) {
                 if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
                 // the host returns on this word, without waiting for the launch to retire
                 __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
+    }
+    if (!a.host_out) return;
+    // Staged form: once every member has written its shard of my result
+    // slot, the whole grid copies it to my host target; the last workgroup
+    // to finish publishes the completion word.
+    if (threadIdx.x == 0)
+        s_go = wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2);
+    __syncthreads();
+    if (!s_go) return;
+    stage_copy(a.host_out, a.stage_result, a.host_bytes);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketOut)) {
+        if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
+        __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -538,6 +538,23 @@ StageSet *stage_setup(const Coll &c)
     return S.ok ? &S : nullptr;
 }
 
+// host ranges pinned through osgpu_host_register, with their device view
+struct HostReg {
+    char *base;
+    size_t bytes;
+    char *dev;
+};
+std::vector<HostReg> g_hostreg;
+
+void *host_device_view(const void *p, size_t nbytes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    const char *c = (const char *) p;
+    for (const HostReg &r : g_hostreg)
+        if (r.dev && c >= r.base && c + nbytes <= r.base + r.bytes) return r.dev + (c - r.base);
+    return nullptr;
+}
+
 long long g_fused_max = -1;  // -1: from the environment
 
 size_t fused_max_bytes()
@@ -796,17 +813,32 @@ int osgpu_finalize(void)
 
 int osgpu_host_register(void *base, size_t bytes)
 {
-    hipError_t e = hipHostRegister(base, bytes, hipHostRegisterDefault);
+    hipError_t e = hipHostRegister(base, bytes, hipHostRegisterMapped);
     if (e != hipSuccess) {
         set_err("hipHostRegister: %s", hipGetErrorString(e));
         return OSGPU_EHIP;
     }
+    void *dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+        (void) hipGetLastError();
+        dev = nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_hostreg.push_back({(char *) base, bytes, (char *) dev});
     return OSGPU_OK;
 }
 
 int osgpu_host_unregister(void *base)
 {
     hipError_t e = hipHostUnregister(base);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (size_t i = 0; i < g_hostreg.size(); i++)
+            if (g_hostreg[i].base == (char *) base) {
+                g_hostreg.erase(g_hostreg.begin() + (long) i);
+                break;
+            }
+    }
     if (e != hipSuccess) {
         set_err("hipHostUnregister: %s", hipGetErrorString(e));
         return OSGPU_EHIP;

@@ -170,6 +170,10 @@ struct SyncSet {
 };
 SyncSet *sync_setup(const Coll &c);
 
+// Device view of host memory inside a range pinned with
+// osgpu_host_register, or nullptr.
+void *host_device_view(const void *p, size_t nbytes);
+
 // Per-PE byte limit of the fused path: osgpu_set_fused_max_bytes, else
 // OSGPU_FUSED_MAX_BYTES, else 1 MiB; 0 = fused path off.
 size_t fused_max_bytes();

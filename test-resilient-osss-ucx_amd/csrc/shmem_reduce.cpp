@@ -203,7 +203,8 @@ void fused_wait(const Call &c, const SyncSet &S, hipStream_t st, unsigned long l
 // team = true: owner-computes over every member's target (srcs/dsts in
 // active-set order); false: pull form, my own target from every source.
 void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
-               const std::vector<void *> &dsts, bool team)
+               const std::vector<void *> &dsts, bool team, const StageSet *G = nullptr,
+               const void *host_in = nullptr, void *host_out = nullptr)
 {
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
@@ -212,7 +213,9 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     memset(&a, 0, sizeof(a));
     long long lo = 0, hi = c.nreduce;
     if (team) osgpu_shard_range(c.nreduce, P, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
-    const bool overlap = !team && ranges_overlap(c.target, c.source, c.nbytes);
+    // (staged form: target and source may overlap -- the source is copied
+    // into staging before any member writes, the target after all are done)
+    const bool overlap = !G && !team && ranges_overlap(c.target, c.source, c.nbytes);
     void *out = overlap ? device_scratch(c.name, c.me, c.nbytes) : c.target;
     for (int i = 0; i < P; i++) {
         a.src[i] = (const char *) srcs[i] + (size_t) lo * s;
@@ -238,9 +241,16 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     a.P = P;
     a.me = idx;
     a.max_blocks = S.max_blocks;
-    t_last_path = team ? OSGPU_RAN_FUSED_TEAM : OSGPU_RAN_FUSED_PULL;
+    if (G) {
+        a.host_in = host_in;
+        a.host_out = host_out;
+        a.stage_mine = G->in(idx, 0);
+        a.stage_result = G->out(idx, 0);
+        a.host_bytes = c.nbytes;
+    }
+    t_last_path = G ? OSGPU_RAN_FUSED_STAGED : team ? OSGPU_RAN_FUSED_TEAM : OSGPU_RAN_FUSED_PULL;
     DBG("%s PE %d: fused %s path, epoch %llu, [%lld, %lld)", c.name, c.me,
-        team ? "team" : "pull", a.epoch, lo, hi);
+        G ? "staged" : team ? "team" : "pull", a.epoch, lo, hi);
     // OSGPU_FUSED_TRACE=1: phase clocks of workgroup 0 / the last workgroup
     static unsigned long long *trace = [] {
         unsigned long long *p = nullptr;
@@ -496,8 +506,25 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
             fatal(name, "no GPU visible: the combine runs only on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
         StageSet *S = getmem_only ? nullptr : stage_setup(c);
-        if (S) run_staged(c, *S);
-        else run_host(c);
+        // small calls on host heaps pinned with osgpu_host_register (on every
+        // PE, like the heap itself): H2D, exchange and D2H in one launch
+        void *hin = nullptr, *hout = nullptr;
+        SyncSet *Y = nullptr;
+        if (S && fused_eligible(c, true) && c.nbytes <= S->slot &&
+            (hin = host_device_view(source, c.nbytes)) &&
+            (hout = host_device_view(target, c.nbytes)) && (Y = sync_setup(c))) {
+            std::vector<const void *> srcs(c.PE_size);
+            std::vector<void *> dsts(c.PE_size);
+            for (int i = 0; i < c.PE_size; i++) {
+                srcs[i] = S->in(i, 0);
+                dsts[i] = S->out(i, 0);
+            }
+            run_fused(c, *Y, srcs, dsts, true, S, hin, hout);
+        } else if (S) {
+            run_staged(c, *S);
+        } else {
+            run_host(c);
+        }
         return;
     }
     int cur = 0;

@@ -32,7 +32,7 @@ CTYPE = {
 PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
 # enum osgpu_ran: what osgpu_last_path() reports
 RAN = ["none", "team", "pull", "rccl", "staged", "getmem", "fused_team", "fused_pull",
-       "barrier_only"]
+       "barrier_only", "fused_staged"]
 
 
 def has_op(t: str, op: str) -> bool:

@@ -22,6 +22,9 @@ modes
         device-side barriers between processes; per-PE SHA-256 and the path
         taken are written for the parent; then calls around a 64 KiB fused
         limit are checked against the oracle
+  goldenhost  the same golden cases on host heaps (the shared-memory
+        symmetric heap, pinned on every PE): small calls take the fused staged
+        path (H2D, exchange and D2H in one launch), larger ones STAGED
   latency  GPU, same setup: per-call time of shmem_int_sum_to_all, fused
         path vs host barriers (bench/tool use)
 usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. \
@@ -103,7 +106,7 @@ def device_heap_modes(L, PES, mode, rank, world):
             assert base, L.osgpu_last_error().decode()
             mapped.append(base)
         assert L.osgpu_heap_register(pe, ctypes.c_void_p(base), H) == 0
-    psync = PES.pes_heap(rank) + (1 << 24) - 8192
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192  # top of the shm heap
     PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     sync = lambda: PES.pes_barrier(0, 0, world, None)  # noqa: E731
     wrk = (ctypes.c_byte * 4096)()
@@ -115,8 +118,13 @@ def device_heap_modes(L, PES, mode, rank, world):
         if raw.size:
             heap[off:off + raw.size].copy_(torch.from_numpy(raw.copy()).cuda())
 
-    if mode == "golden":
+    if mode in ("golden", "goldenhost"):
         digests, paths = {}, {}
+        host = mode == "goldenhost"
+        if host:  # the shared-memory symmetric heap, pinned on every PE
+            hbase = PES.pes_heap(rank)
+            hbytes = (1 << 26) - (1 << 16)
+            assert L.osgpu_host_register(ctypes.c_void_p(hbase), hbytes) == 0
         for ci, c in enumerate(O.load_cases()):
             if c["npes"] > world:
                 continue
@@ -124,19 +132,32 @@ def device_heap_modes(L, PES, mode, rank, world):
             s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
             act = O.active_set(c["PE_start"], c["logPE_stride"], c["PE_size"])
             toff = max(4096, (n * s + 4095) // 4096 * 4096)
+            if host and 2 * toff > hbytes:
+                continue
             if rank < c["npes"]:
-                put(0, O.case_inputs(c)[rank])
+                if host:
+                    raw = np.ascontiguousarray(O.case_inputs(c)[rank]).view(np.uint8).reshape(-1)
+                    ctypes.memmove(hbase, raw.ctypes.data, raw.size)
+                else:
+                    put(0, O.case_inputs(c)[rank])
             fn = getattr(L, f"shmem_{t}_{op}_to_all")
-            for path in (osgpu.PATH_AUTO, osgpu.PATH_PULL):
+            for path in ((osgpu.PATH_AUTO,) if host else (osgpu.PATH_AUTO, osgpu.PATH_PULL)):
                 L.osgpu_set_path(path)
-                heap[toff:toff + max(n * s, 16)].fill_(0xA5)
-                torch.cuda.synchronize()
+                if host:
+                    ctypes.memset(hbase + toff, 0xA5, max(n * s, 16))
+                else:
+                    heap[toff:toff + max(n * s, 16)].fill_(0xA5)
+                    torch.cuda.synchronize()
                 sync()
                 if rank in act:
-                    fn(dev0 + toff, dev0, n, c["PE_start"], c["logPE_stride"], c["PE_size"],
+                    b0 = hbase if host else dev0
+                    fn(b0 + toff, b0, n, c["PE_start"], c["logPE_stride"], c["PE_size"],
                        wrk, psync)
                     paths[f"{ci}/{path}"] = osgpu.last_path()
-                    got = heap[toff:toff + n * s].cpu().numpy()
+                    if host:
+                        got = np.frombuffer(ctypes.string_at(hbase + toff, n * s), np.uint8)
+                    else:
+                        got = heap[toff:toff + n * s].cpu().numpy()
                     if t == "longdouble":
                         got = got.reshape(-1, 16)[:, :10].reshape(-1)
                     digests[f"{ci}/{path}"] = O.digest(O.from_value_bytes(t, got))
@@ -144,6 +165,9 @@ def device_heap_modes(L, PES, mode, rank, world):
                 sync()
         L.osgpu_set_path(osgpu.PATH_AUTO)
         res["digests"], res["paths"] = digests, paths
+        if host:
+            assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
+    if mode == "golden":
         # around a 64 KiB fused limit: under, at, just over
         lim = 64 << 10
         L.osgpu_set_fused_max_bytes(lim)
@@ -215,6 +239,28 @@ def device_heap_modes(L, PES, mode, rank, world):
                                       "gpu_us_median": float(np.median(gpu)),
                                       "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
                                       "path": ran, "correct": ok}
+            # host symmetric heap (the shared-memory heap, pinned): pipelined
+            # STAGED path vs the fused one-launch staged path
+            hbase = PES.pes_heap(rank)
+            src_h = np.ctypeslib.as_array((ctypes.c_int32 * n).from_address(hbase))
+            src_h[:] = np.arange(n, dtype=np.int32) + rank
+            assert L.osgpu_host_register(ctypes.c_void_p(hbase), 1 << 23) == 0
+            for name, lim in (("host_staged", 0), ("host_fused_staged", 1 << 30)):
+                L.osgpu_set_fused_max_bytes(lim)
+                ts = []
+                for r in range(reps + 5):
+                    sync()
+                    t0 = time.perf_counter()
+                    L.shmem_int_sum_to_all(hbase + toff, hbase, n, 0, 0, world, wrk, psync)
+                    sync()
+                    ts.append(time.perf_counter() - t0)
+                got = np.ctypeslib.as_array((ctypes.c_int32 * n).from_address(hbase + toff))
+                ok = bool(np.array_equal(got, world * np.arange(n, dtype=np.int32)
+                                         + world * (world - 1) // 2))
+                lat[f"{n}/{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
+                                      "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
+                                      "path": osgpu.last_path(), "correct": ok}
+            assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
         L.osgpu_set_fused_max_bytes(-1)
         L.osgpu_set_path(osgpu.PATH_AUTO)
         res["latency"] = lat
@@ -232,10 +278,10 @@ def main():
     L = osgpu.load()
     counter = [0]
     PES = None
-    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in ("hoststaged", "hostcoll",
-                                                                     "golden", "latency"):
+    if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
+            "hoststaged", "hostcoll", "golden", "goldenhost", "latency"):
         from support import peshm
-        PES = peshm.init(rank, world, 1 << 24, dist)
+        PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
     else:
         ops, keep = pe_ops(rank, world, counter)
@@ -255,18 +301,30 @@ def main():
             # symmetric pSync at the top of the shared heap (the staged path
             # exchanges its staging-buffer handles through spare pSync words)
             psync = base + (1 << 24) - 4096
-            for hp, inplace in (("staged", False), ("staged", True), ("getmem", False)):
-                os.environ["OSGPU_HOST_PATH"] = hp
-                ctypes.memmove(base, raw.ctypes.data, raw.size)
-                tgt = base + (0 if inplace else toff)
-                wrk = (ctypes.c_byte * 4096)()
-                getattr(L, f"shmem_{t}_{op}_to_all")(tgt, base, n, 0, 0, world, wrk, psync)
-                got = np.frombuffer(ctypes.string_at(tgt, n * s), dtype=np.uint8)
-                if t == "longdouble":
-                    got = got.reshape(-1, 16)[:, :10].reshape(-1)
-                out[f"{t}/{op}/{hp}/{int(inplace)}"] = got.tobytes().hex()
-                assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
-                dist.barrier()
+            # pinned: the heap registered on every PE (osgpu_host_register) --
+            # small calls then run the fused one-launch staged path
+            for pinned in (False, True):
+                if pinned:
+                    assert L.osgpu_host_register(ctypes.c_void_p(base), 1 << 24) == 0
+                for hp, inplace, fused in (("staged", False, -1), ("staged", True, -1),
+                                           ("staged", False, 0), ("getmem", False, -1)):
+                    os.environ["OSGPU_HOST_PATH"] = hp
+                    L.osgpu_set_fused_max_bytes(fused)
+                    ctypes.memmove(base, raw.ctypes.data, raw.size)
+                    tgt = base + (0 if inplace else toff)
+                    wrk = (ctypes.c_byte * 4096)()
+                    getattr(L, f"shmem_{t}_{op}_to_all")(tgt, base, n, 0, 0, world, wrk, psync)
+                    key = f"{t}/{op}/{hp}/{int(inplace)}/{fused}/{int(pinned)}"
+                    res.setdefault("paths", {})[key] = osgpu.last_path()
+                    got = np.frombuffer(ctypes.string_at(tgt, n * s), dtype=np.uint8)
+                    if t == "longdouble":
+                        got = got.reshape(-1, 16)[:, :10].reshape(-1)
+                    out[key] = got.tobytes().hex()
+                    assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
+                    dist.barrier()
+                if pinned:
+                    assert L.osgpu_host_unregister(ctypes.c_void_p(base)) == 0
+            L.osgpu_set_fused_max_bytes(-1)
         for hp in ("staged", "getmem"):
             os.environ["OSGPU_HOST_PATH"] = hp
             run_colls(L, rank, world, base, base + (1 << 22), psync, out, hp,
@@ -274,7 +332,7 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
-    if mode in ("golden", "latency"):
+    if mode in ("golden", "goldenhost", "latency"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096

@@ -145,6 +145,16 @@ def test_host_staged_processes(tmp_path, world, monkeypatch):
              ("long", "or", 65, "or"), ("complexf", "prod", 1000, "edge"),
              ("longdouble", "min", 333, "edge"))
     _check_specs(res, specs, 0xDEF)
+    # small calls on a pinned heap: the fused one-launch staged path
+    for r in range(world):
+        for key, ran in res[r]["paths"].items():
+            t, op, hp, inplace, fused, pinned = key.split("/")
+            n = next(sp[2] for sp in specs if sp[0] == t and sp[1] == op)
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            small = fused == "-1" and t != "longdouble" and n * s <= (1 << 20)
+            want = ("getmem" if hp == "getmem" else
+                    "fused_staged" if pinned == "1" and small else "staged")
+            assert ran == want, (key, r, ran)
     _check_colls(res, "staged")
     _check_colls(res, "getmem")
 
@@ -188,3 +198,37 @@ def test_fused_path_golden_processes(tmp_path):
         for key, (exact, ran, fused) in res[r]["boundary"].items():
             assert exact, (key, r)
             assert ran.startswith("fused_") == fused, (key, r, ran)
+
+
+@pytest.mark.gpu
+def test_fused_staged_golden_processes(tmp_path):
+    """The golden cases with at most 4 PEs on HOST symmetric heaps (the
+    reference's placement: a shared-memory heap, pinned on every PE), four
+    processes on cuda:0.  Calls of at most 1 MiB per PE (not long double)
+    run as one launch that copies the source in over PCIe, exchanges on the
+    GPU and copies the target out; larger ones take the pipelined STAGED
+    path.  Every member's target bit-exact against the reference digests."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 4
+    res = launch("goldenhost", world, tmp_path)
+    cases = O.load_cases()
+    nfused = nchecked = 0
+    for r in range(world):
+        for key, dg in res[r]["digests"].items():
+            c = cases[int(key.split("/")[0])]
+            assert dg == c["digests"][str(r)], (c["type"], c["op"], c["npes"], c["nreduce"],
+                                                c["tag"], r)
+            nchecked += 1
+            s = 16 if c["type"] == "longdouble" else np.dtype(O.NP_DTYPE[c["type"]]).itemsize
+            ran = res[r]["paths"][key]
+            if c["nreduce"] == 0:
+                want = "barrier_only"
+            elif c["type"] != "longdouble" and c["PE_size"] >= 2 and c["nreduce"] * s <= 1 << 20:
+                want = "fused_staged"
+            else:
+                want = "staged"
+            assert ran == want, (key, r, ran, want)
+            nfused += ran == "fused_staged"
+    assert nchecked > 1000 and nfused > 700, (nchecked, nfused)
