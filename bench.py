@@ -43,6 +43,7 @@ for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec, MI355X_MICROARCH.md
+XGMI_LINK_GBS = 76.8           # MI355X xGMI: 153.6 GB/s bidirectional per peer link
 GIB = float(1 << 30)
 METRIC = "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2/4/8 GPU"
 
@@ -538,6 +539,18 @@ def bench_multi(args):
         res["ms_per_step"] = t / args.steps * 1e3
         res["config"]["path"] = "p2p-team (exact owner-computes kernel over IPC-mapped HBM, xGMI)"
         res["config"]["algbw_GiBs"] = n * 8 * args.steps / t / GIB
+        # the exchange is link-bound: per step every GPU pulls n*8/P bytes
+        # from each of its P-1 peers and pushes as many back, one xGMI link
+        # per peer (the traffic of a reduce-scatter + all-gather)
+        per_dir = (world - 1) * (n * 8 // world) * args.steps / t / 1e9
+        peak = (world - 1) * XGMI_LINK_GBS
+        res["roofline"] = {
+            "bound": "xgmi", "achieved": per_dir, "peak": peak, "unit": "GB/s",
+            "frac": per_dir / peak, "traffic": None,
+            "kernel": f"osgpu::team_vec_kernel<double, SUM, {world}>",
+            "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
+                     f"second (it sends as many); peak = {world - 1} x {XGMI_LINK_GBS} GB/s per "
+                     f"direction (MI355X xGMI, 153.6 GB/s bidirectional per link)")}
         res["parity_sample"] = _sample_parity(rank, world, src, tgt, n, "sum", dist)
         _log(rank, "team done")
     else:
