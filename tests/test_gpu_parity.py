@@ -230,6 +230,43 @@ def test_longdouble_8byte_aligned_arrays(torch_cuda, op):
     assert np.array_equal(got, O.value_bytes(want).reshape(-1))
 
 
+@pytest.mark.parametrize("device", [True, False], ids=["device", "host"])
+def test_active_sets_beyond_eight_pes(torch_cuda, device):
+    """12 PEs (threads), the whole job and a 10-PE subset: past the team
+    kernel's 8 members the device path is the pull form with the fold
+    chained over launches of at most 8 inputs (combine.hip launch_op), the
+    host path every PE folding its own staged chunk.  Bit-exact per PE."""
+    from support import team as T
+    npes = 12
+    tm = T.Team(npes, 2 * 4097 * 16 + 8192, device=device)
+    try:
+        for t, op, dist_ in (("double", "sum", "wide"), ("float", "prod", "wide"),
+                             ("int", "xor", "bits"), ("complexd", "prod", "edge"),
+                             ("longdouble", "max", "edge"), ("short", "sum", "bits")):
+            s = 16 if t == "longdouble" else O.NP_DTYPE[t]().itemsize
+            for n in (1000, 4097):
+                for start, size in ((0, 12), (2, 10)):
+                    src = O.team_inputs(t, npes, n, 0x1200 + n + start, dist_)
+                    want = O.to_all(t, op, src, start, 0, size)
+                    toff = tgt_off(n * s)
+                    for pe in range(npes):
+                        tm.write(pe, 0, src[pe])
+                        tm.fill(pe, toff, n * s, 0x3C)
+                    tm.run(t, op, toff, 0, n, start, 0, size)
+                    for pe in range(npes):
+                        raw = tm.read(pe, toff, n * s)
+                        if want[pe] is None:
+                            assert (raw == 0x3C).all(), (t, op, n, start, pe)
+                            continue
+                        if t == "longdouble":
+                            raw = raw.reshape(-1, 16)[:, :10].reshape(-1)
+                        assert np.array_equal(raw, O.value_bytes(want[pe]).reshape(-1)), \
+                            (t, op, n, start, size, pe)
+    finally:
+        tm.lib.osgpu_finalize()
+        team(device)  # restore the shared 8-PE team for the other tests
+
+
 def test_large_config2_shape_properties(torch_cuda):
     """BASELINE config 2 at full size (nreduce = 64 Mi doubles, 2 inputs):
     checked against the oracle on a strided sample and through the exact
