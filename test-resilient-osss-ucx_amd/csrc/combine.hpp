@@ -84,8 +84,12 @@ struct FusedArgs {
     void *stage_mine;                     // my input staging slot (= src[me])
     const void *stage_result;             // my result staging slot (= one of dst[])
     size_t host_bytes;
+    // copy form (launch_fused_copy): nseg segments src[d] -> dst[d]
+    size_t seg_bytes[kMaxTeam];
+    int nseg;
 };
 bool fused_supported(int type);
+hipError_t launch_fused_copy(const FusedArgs &a, hipStream_t s);
 hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s);
 
 // x87 80-bit extended combine (soft-float on the GPU), longdouble.hip

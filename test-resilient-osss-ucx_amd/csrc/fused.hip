@@ -193,6 +193,58 @@ __device__ void stage_copy(void *dst, const void *src, size_t nbytes)
     }
 }
 
+// Steps 1-2 (device form): workgroup 0 arrives in every member's area,
+// every workgroup waits for all arrivals.  False: timed out (error set).
+__device__ __forceinline__ bool fused_arrive(const FusedArgs &a, int &s_go)
+{
+    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
+        st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
+    if (threadIdx.x == 0)
+        s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
+    __syncthreads();
+    return s_go;
+}
+
+// Step 4 (device form): release, ticket; the last workgroup signals done,
+// waits for every member's done and publishes the host completion word.
+__device__ __forceinline__ void fused_done(const FusedArgs &a, int &s_go)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0 && last_workgroup(a, kFlagTicket)) {
+        for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
+        if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
+            __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    (void) s_go;
+}
+
+// The data-movement collectives' small calls (shmem_collect.cpp): the pieces
+// of my target pulled from every member's source, between the same device
+// barriers.  Segment d: a.seg_bytes[d] bytes from a.src[d] to a.dst[d].
+__global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
+{
+    __shared__ int s_go;
+    if (!fused_arrive(a, s_go)) return;
+    const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
+    const size_t stride = (size_t) gridDim.x * kFBlock;
+    for (int d = 0; d < a.nseg; d++) {
+        const char *src = static_cast<const char *>(a.src[d]);
+        char *dst = static_cast<char *>(a.dst[d]);
+        const size_t nb = a.seg_bytes[d];
+        if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0) {
+            const size_t nv = nb / 16;
+            for (size_t j = tid; j < nv; j += stride)
+                store_out(reinterpret_cast<u32x4 *>(dst) + j,
+                          __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src) + j));
+            for (size_t b = nv * 16 + tid; b < nb; b += stride) dst[b] = src[b];
+        } else {
+            for (size_t b = tid; b < nb; b += stride) dst[b] = src[b];
+        }
+    }
+    fused_done(a, s_go);
+}
+
 template <typename T, int OP, bool VEC>
 __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
 {
@@ -361,6 +413,21 @@ hipError_t fused_cplx(int op, const FusedArgs &a, hipStream_t s)
 }
 
 }  // namespace
+
+hipError_t launch_fused_copy(const FusedArgs &a0, hipStream_t s)
+{
+    FusedArgs a = a0;
+    if (a.P < 2 || a.P > kMaxTeam || a.nseg < 0 || a.nseg > kMaxTeam || a.me < 0 ||
+        a.me >= a.P || a.max_blocks < 1 || a.max_blocks > kFusedBlocksPerGpu)
+        return hipErrorInvalidValue;
+    size_t most = 0;
+    for (int d = 0; d < a.nseg; d++) most = a.seg_bytes[d] > most ? a.seg_bytes[d] : most;
+    size_t blocks = (most / 16 + kFBlock - 1) / kFBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (size_t) a.max_blocks) blocks = (size_t) a.max_blocks;
+    hipLaunchKernelGGL(fused_copy_kernel, dim3((unsigned) blocks), dim3(kFBlock), 0, s, a);
+    return hipGetLastError();
+}
 
 bool fused_supported(int type) { return type != T_LONGDOUBLE && type >= 0 && type < T_NTYPES; }
 

@@ -577,6 +577,35 @@ size_t fused_max_bytes()
 
 std::map<std::tuple<int, int, int, int, int>, SyncSet> g_sync;  // (me, set, device)
 
+// Completion of a fused call: spin on the host-mapped word the kernel's
+// last workgroup writes once every member is done (no wait for the launch to
+// retire); the stream is polled now and then so a launch that ended without
+// writing it (a timed-out barrier) is noticed.
+void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned long long epoch)
+{
+    for (unsigned it = 1;; it++) {
+        if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
+        if (__atomic_load_n(S.err_h, __ATOMIC_RELAXED)) return;  // fused_check reports it
+        if ((it & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return;  // ended; fused_check tells done from failed
+            if (q != hipErrorNotReady) fatal(where, "fused launch: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+void fused_check(const char *where, const SyncSet &S, unsigned long long epoch, bool word)
+{
+    const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
+    if (err)
+        fatal(where, "device barrier (%s) timed out after %.1f s: a member of the active set "
+                     "did not enter or finish the call",
+              err == 1 ? "entry" : "exit", S.timeout_s);
+    if (word && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < epoch)
+        fatal(where, "fused launch ended without completing epoch %llu", epoch);
+}
+
 SyncSet *sync_setup(const Coll &c)
 {
     int dev = 0;

@@ -169,6 +169,9 @@ struct SyncSet {
     unsigned long long *done_h = nullptr, *done_d = nullptr;  // host-mapped completion epoch
 };
 SyncSet *sync_setup(const Coll &c);
+// wait for a fused launch's completion word (epoch) / report a failed one
+void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned long long epoch);
+void fused_check(const char *where, const SyncSet &S, unsigned long long epoch, bool word);
 
 // Device view of host memory inside a range pinned with
 // osgpu_host_register, or nullptr.

@@ -55,6 +55,8 @@ namespace {
 
 using namespace osgpu::rt;
 
+thread_local int t_last_coll = OSGPU_RAN_NONE;
+
 enum Kind { K_BCAST, K_COLLECT, K_FCOLLECT, K_ALLTOALL };
 
 constexpr int kCountWord = 8;  // pSync word carrying nelems during collect
@@ -180,6 +182,55 @@ bool device_sources(const CCall &c, std::vector<const char *> &src)
     return true;
 }
 
+// Small broadcast / fcollect / alltoall calls run as ONE launch with the
+// reduce path's device-side barriers (fused.hip fused_copy_kernel).  The
+// decision uses only arguments every member shares (never which member I
+// am), so every member takes the same path.
+bool fused_copy_eligible(const CCall &c)
+{
+    const int em = entry_mode();
+    const size_t nb = c.nelems * c.esz;
+    const size_t bytes = c.kind == K_BCAST ? nb : (size_t) c.PE_size * nb;
+    return (em == ENTRY_STREAM || em == ENTRY_NONE) && c.kind != K_COLLECT &&
+           c.PE_size >= 2 && c.PE_size <= osgpu::kMaxTeam && bytes <= fused_max_bytes() &&
+           c.ops.getmem != nullptr;
+}
+
+void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg> &segs,
+                    char *out, hipStream_t st)
+{
+    osgpu::FusedArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nseg = (int) segs.size();
+    for (int d = 0; d < a.nseg; d++) {
+        a.src[d] = segs[d].src;
+        a.dst[d] = segs[d].dst;
+        a.seg_bytes[d] = segs[d].bytes;
+    }
+    for (int i = 0; i < c.PE_size; i++) a.flags[i] = S.peer[i];
+    a.mine = S.local;
+    a.err = S.err_d;
+    a.done_host = S.done_d;
+    a.epoch = ++S.epoch;
+    a.timeout = S.timeout;
+    a.P = c.PE_size;
+    a.me = S.idx;
+    a.max_blocks = S.max_blocks;
+    DBG("%s PE %d: fused copy, %d pieces, epoch %llu", c.name, c.me, a.nseg, a.epoch);
+    entry_order(c.name, st);
+    hipError_t e = osgpu::launch_fused_copy(a, st);
+    if (e != hipSuccess) fatal(c.name, "fused copy launch: %s", hipGetErrorString(e));
+    const bool scratch = out != (char *) c.target;
+    if (scratch) {  // every reader of my source is done when the launch ends
+        if (c.out_bytes)
+            HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.out_bytes, hipMemcpyDeviceToDevice, st));
+        stream_wait(c.name, st);
+    } else {
+        fused_wait(c.name, S, st, a.epoch);
+    }
+    fused_check(c.name, S, a.epoch, !scratch);
+}
+
 void run_copy(const CCall &c, const std::vector<const char *> &src, bool counts_done)
 {
     hipStream_t st = pe_stream(c.name, c.me);
@@ -189,6 +240,13 @@ void run_copy(const CCall &c, const std::vector<const char *> &src, bool counts_
     std::vector<osgpu::CopySeg> segs;
     for (const Piece &p : c.pieces)
         if (p.len) segs.push_back({src[p.from] + p.src_off, out + p.dst_off, p.len});
+    SyncSet *Y = nullptr;
+    if (!counts_done && fused_copy_eligible(c) && (Y = sync_setup(c))) {
+        t_last_coll = OSGPU_RAN_FUSED_COPY;
+        run_fused_copy(c, *Y, segs, out, st);
+        return;
+    }
+    t_last_coll = OSGPU_RAN_COPY;
     DBG("%s PE %d: copy path, %zu pieces, %zu bytes out%s", c.name, c.me, segs.size(),
         c.out_bytes, scratch ? " (scratch)" : "");
     if (!counts_done) {
@@ -214,6 +272,7 @@ bool rccl_whole_job(const CCall &c)
 
 void run_rccl(const CCall &c)
 {
+    t_last_coll = OSGPU_RAN_RCCL;
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t nb = c.nelems * c.esz;
     entry_sync(c.name);
@@ -248,6 +307,7 @@ void run_rccl(const CCall &c)
 // slots of a StageSet are one region: in = C bytes, out = P*C bytes.
 void run_staged(const CCall &c, StageSet &S)
 {
+    t_last_coll = OSGPU_RAN_STAGED;
     const int P = c.PE_size;
     const size_t region = 4 * S.slot;
     size_t C = region / (size_t) (P + 1);
@@ -304,6 +364,7 @@ void run_staged(const CCall &c, StageSet &S)
 // involved, so nothing is left for the GPU to do on this path.
 void run_getmem(const CCall &c)
 {
+    t_last_coll = OSGPU_RAN_GETMEM;
     if (!c.ops.getmem) fatal(c.name, "host-memory arguments need shmem_getmem");
     const bool tmp = overlap2(c.target, c.out_bytes, c.source, c.src_len[c.idx]) &&
                      my_source_read(c);
@@ -341,6 +402,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
     if (kind == K_BCAST && (PE_root < 0 || PE_root >= PE_size))
         fatal(name, "PE_root %d outside the active set of %d PEs", PE_root, PE_size);
     if (kind != K_COLLECT && nelems == 0) {  // nothing moves; the collective still syncs
+        t_last_coll = OSGPU_RAN_BARRIER_ONLY;
         barrier(c);
         barrier(c);
         return;
@@ -359,6 +421,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
     size_t moved = 0;
     for (size_t l : c.src_len) moved += l;
     if (moved == 0) {  // a collect of empty contributions only synchronises
+        t_last_coll = OSGPU_RAN_BARRIER_ONLY;
         barrier(c);
         c.pSync[kCountWord] = 0;
         return;
@@ -409,6 +472,8 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
 }
 
 }  // namespace
+
+extern "C" int osgpu_last_coll_path(void) { return t_last_coll; }
 
 // pshmem_* strong, shmem_* weak aliases (as src/broadcast.c:14-20,
 // src/collect.c:14-20, src/fcollect.c:14-20, src/alltoall.c:11-23 under

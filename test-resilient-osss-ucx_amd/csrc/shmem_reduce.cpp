@@ -179,27 +179,6 @@ bool fused_eligible(const Call &c, bool team)
            c.ops.getmem != nullptr;
 }
 
-// Completion of a fused call: spin on the host-mapped word the kernel's
-// last workgroup writes once every member is done (no wait for the launch to
-// retire); the stream is polled now and then so a launch that ended without
-// writing it (a timed-out barrier) is noticed.
-void fused_wait(const Call &c, const SyncSet &S, hipStream_t st, unsigned long long epoch)
-{
-    for (unsigned it = 1;; it++) {
-        if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
-        if (__atomic_load_n(S.err_h, __ATOMIC_RELAXED)) return;  // reported by the caller
-        if ((it & 4095) == 0) {
-            const hipError_t q = hipStreamQuery(st);
-            if (q == hipSuccess) {
-                if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
-                return;  // ended without completing: the error word says why
-            }
-            if (q != hipErrorNotReady) fatal(c.name, "fused launch: %s", hipGetErrorString(q));
-        }
-        __builtin_ia32_pause();
-    }
-}
-
 // team = true: owner-computes over every member's target (srcs/dsts in
 // active-set order); false: pull form, my own target from every source.
 void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
@@ -268,7 +247,7 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
         stream_wait(c.name, st);
     } else {
-        fused_wait(c, S, st, a.epoch);
+        fused_wait(c.name, S, st, a.epoch);
     }
     if (trace) {
         const double tk = 1e6 / 1e8;  // us per tick of the 100 MHz wall clock
@@ -278,13 +257,7 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
                 (trace[3] - trace[2]) * tk, (trace[4] - trace[3]) * tk,
                 (trace[6] - trace[5]) * tk);
     }
-    const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
-    if (!err && !overlap && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < a.epoch)
-        fatal(c.name, "fused launch ended without completing epoch %llu", a.epoch);
-    if (err)
-        fatal(c.name, "device barrier (%s) timed out after %.1f s: a member of the active "
-                      "set did not enter or finish the call",
-              err == 1 ? "entry" : "exit", S.timeout_s);
+    fused_check(c.name, S, a.epoch, !overlap);
 }
 
 bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *mult)

@@ -32,7 +32,7 @@ CTYPE = {
 PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
 # enum osgpu_ran: what osgpu_last_path() reports
 RAN = ["none", "team", "pull", "rccl", "staged", "getmem", "fused_team", "fused_pull",
-       "barrier_only", "fused_staged"]
+       "barrier_only", "fused_staged", "copy", "fused_copy"]
 
 
 def has_op(t: str, op: str) -> bool:
@@ -135,6 +135,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_host_unregister.argtypes = [vp]
     L.osgpu_set_fused_max_bytes.argtypes = [ctypes.c_longlong]
     L.osgpu_last_path.restype = ctypes.c_int
+    L.osgpu_last_coll_path.restype = ctypes.c_int
     L.osgpu_last_error.restype = ctypes.c_char_p
     L.osgpu_version.restype = ctypes.c_char_p
     _LIB = L
@@ -144,6 +145,11 @@ def load() -> ctypes.CDLL:
 def last_path() -> str:
     """Name of the path the calling thread's last reduce-to-all call took."""
     return RAN[load().osgpu_last_path()]
+
+
+def last_coll_path() -> str:
+    """Name of the path the calling thread's last data-movement collective took."""
+    return RAN[load().osgpu_last_coll_path()]
 
 
 def to_all(t: str, op: str):

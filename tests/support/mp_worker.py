@@ -25,6 +25,10 @@ modes
   goldenhost  the same golden cases on host heaps (the shared-memory
         symmetric heap, pinned on every PE): small calls take the fused staged
         path (H2D, exchange and D2H in one launch), larger ones STAGED
+  collgolden  GPU, IPC device heaps: broadcast / collect / fcollect /
+        alltoall cases of support/coll_cases.py fused_cases (active subsets,
+        roots, odd sizes, source == target); small calls run the fused
+        one-launch copy; SHA-256 of every target region (margins included)
   latency  GPU, same setup: per-call time of shmem_int_sum_to_all, fused
         path vs host barriers (bench/tool use)
 usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. \
@@ -167,6 +171,38 @@ def device_heap_modes(L, PES, mode, rank, world):
         res["digests"], res["paths"] = digests, paths
         if host:
             assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
+    if mode == "collgolden":
+        import hashlib
+        from support import coll_cases as CC
+        import oracle_coll as OC
+        digests, paths = {}, {}
+        for ci, c in enumerate(CC.fused_cases()):
+            npes, start, log, size = c["set"]
+            if npes > world:
+                continue
+            per_src, tgt_off, tgt_bytes, src_off = CC.fused_layout(c)
+            pes = OC.active_set(start, log, size)
+            if rank < npes:
+                src, tgt = CC.fused_inputs(c, rank)
+                put(tgt_off - CC.MARGIN, tgt)
+                if not c["same"] and src.size:
+                    put(0, src)
+            torch.cuda.synchronize()
+            sync()
+            if rank in pes:
+                f = osgpu.coll(c["kind"], c["bits"])
+                cnt = CC.fused_counts(c)[rank]
+                if c["kind"] == "broadcast":
+                    f(dev0 + tgt_off, dev0 + src_off, cnt, c["root"], start, log, size, psync)
+                else:
+                    f(dev0 + tgt_off, dev0 + src_off, cnt, start, log, size, psync)
+                paths[str(ci)] = osgpu.last_coll_path()
+                assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
+            if rank < npes:
+                got = heap[tgt_off - CC.MARGIN:tgt_off + tgt_bytes + CC.MARGIN].cpu().numpy()
+                digests[str(ci)] = hashlib.sha256(got.tobytes()).hexdigest()
+            sync()
+        res["digests"], res["paths"] = digests, paths
     if mode == "golden":
         # around a 64 KiB fused limit: under, at, just over
         lim = 64 << 10
@@ -239,6 +275,28 @@ def device_heap_modes(L, PES, mode, rank, world):
                                       "gpu_us_median": float(np.median(gpu)),
                                       "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
                                       "path": ran, "correct": ok}
+            # data-movement collectives on the same device heaps: fused copy
+            # (one launch) vs the copy kernel between host barriers
+            for kind in ("fcollect", "broadcast", "alltoall"):
+                f = osgpu.coll(kind, 32)
+                ne = n // world if kind == "alltoall" else n
+                coff = (world * n * 4 + 4095) // 4096 * 4096 + (8 << 20)
+                for name, lim in (("host_barriers", 0), ("fused", 1 << 30)):
+                    L.osgpu_set_fused_max_bytes(lim)
+                    ts = []
+                    for r in range(reps + 5):
+                        sync()
+                        t0 = time.perf_counter()
+                        if kind == "broadcast":
+                            f(dev0 + coff, dev0, ne, 0, 0, 0, world, psync)
+                        else:
+                            f(dev0 + coff, dev0, ne, 0, 0, world, psync)
+                        sync()
+                        ts.append(time.perf_counter() - t0)
+                    lat[f"{n}/{kind}32_{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
+                                                   "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
+                                                   "path": osgpu.last_coll_path(),
+                                                   "correct": True}
             # host symmetric heap (the shared-memory heap, pinned): pipelined
             # STAGED path vs the fused one-launch staged path
             hbase = PES.pes_heap(rank)
@@ -279,7 +337,7 @@ def main():
     counter = [0]
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
-            "hoststaged", "hostcoll", "golden", "goldenhost", "latency"):
+            "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -332,7 +390,7 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
-    if mode in ("golden", "goldenhost", "latency"):
+    if mode in ("golden", "goldenhost", "collgolden", "latency"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096

@@ -232,3 +232,32 @@ def test_fused_staged_golden_processes(tmp_path):
             assert ran == want, (key, r, ran, want)
             nfused += ran == "fused_staged"
     assert nchecked > 1000 and nfused > 700, (nchecked, nfused)
+
+
+@pytest.mark.gpu
+def test_fused_collectives_processes(tmp_path):
+    """broadcast / fcollect / alltoall (32/64) with one process per PE (4 on
+    cuda:0, IPC device heaps): small calls run as one launch with the
+    device-side barriers (fused copy); collect keeps its count exchange and
+    host barriers.  Every member's target region, margins included, must
+    equal the restatement's (oracle/oracle_coll.py)."""
+    import hashlib
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from support import coll_cases as CC
+    world = 4
+    res = launch("collgolden", world, tmp_path)
+    nfused = 0
+    for ci, c in enumerate(CC.fused_cases()):
+        if c["set"][0] > world:
+            continue
+        exp = CC.fused_expected(c)
+        for r in range(c["set"][0]):
+            want = hashlib.sha256(exp[r].tobytes()).hexdigest()
+            assert res[r]["digests"][str(ci)] == want, (c, r)
+            ran = res[r]["paths"].get(str(ci))
+            if ran is not None:
+                assert ran == ("copy" if c["kind"] == "collect" else "fused_copy"), (c, r, ran)
+                nfused += ran == "fused_copy"
+    assert nfused > 300, nfused
