@@ -200,6 +200,60 @@ def api_call_time(n, reps=20):
     return out
 
 
+def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
+    """Median HIP-event time of osgpu_combine(K = 2) on its own stream over
+    n elements of two resident inputs; (K + 1) * n * esz bytes per launch."""
+    dev = torch.device("cuda:0")
+    a = torch.empty(n, dtype=dtype, device=dev)
+    b = torch.empty(n, dtype=dtype, device=dev)
+    fill(a, 1)
+    fill(b, 2)
+    out = torch.empty(n, dtype=dtype, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
+    sp = ctypes.c_void_p(st.cuda_stream)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        assert L.osgpu_combine(type_code, op_code, out.data_ptr(), srcs, 2, n, sp) == 0
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record(st)
+        L.osgpu_combine(type_code, op_code, out.data_ptr(), srcs, 2, n, sp)
+        e1.record(st)
+    torch.cuda.synchronize()
+    ts = sorted(e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev)
+    return ts[len(ts) // 2], a, b, out
+
+
+def extra_kernel_rates(L, torch):
+    """The north-star statement (double sum at nreduce = 128 Mi: >= 80 % of
+    HBM READ bandwidth) and BASELINE config 3 (long and/or/xor, 256 MiB per
+    array = 32 Mi elements, bit-exact), on the same combine kernel."""
+    out = {}
+    n = 128 << 20
+    t, a, b, o = kernel_rate(L, torch, 5, 0, n, 8, torch.float64,
+                             lambda x, k: x.uniform_(1.0, 2.0))
+    out["north_star_double_sum_128Mi"] = {
+        "kernel_us": t * 1e6, "read_GBs": 2 * n * 8 / t / 1e9,
+        "read_frac_of_8TBs": 2 * n * 8 / t / 8e12, "frac_all_bytes": 3 * n * 8 / t / 8e12}
+    del a, b, o
+    torch.cuda.empty_cache()
+    n = 32 << 20
+    c3 = {"nreduce": n, "bytes_per_array": n * 8}
+    for name, code, ref in (("and", 2, lambda x, y: x & y), ("or", 3, lambda x, y: x | y),
+                            ("xor", 4, lambda x, y: x ^ y)):
+        t, a, b, o = kernel_rate(L, torch, 2, code, n, 8, torch.int64,
+                                 lambda x, k: x.random_(-(1 << 62), 1 << 62))
+        c3[name] = {"kernel_us": t * 1e6, "GBs": 3 * n * 8 / t / 1e9,
+                    "frac_of_8TBs": 3 * n * 8 / t / 8e12,
+                    "bit_exact": bool(torch.equal(o, ref(a, b)))}
+        del a, b, o
+    torch.cuda.empty_cache()
+    out["config3_long_bitwise_256MiB"] = c3
+    return out
+
+
 def small_call_latency(n=1024, reps=300):
     """BASELINE config 1's shape (shmem_int_sum_to_all, nreduce = 1 Ki, 2 PEs)
     with one PROCESS per PE, both on this GPU (IPC device heaps, the
@@ -285,6 +339,12 @@ def bench_single(args):
                                "device-resident combine kernel",
                    "nreduce": n, "K": 2, "bytes_per_step": B},
     }
+    del a, b, out
+    torch.cuda.empty_cache()
+    try:
+        res.update(extra_kernel_rates(L, torch))
+    except Exception as e:  # report, never hide
+        res["extra_kernels"] = {"error": repr(e)}
     tr = load_traffic()
     res["roofline"] = {
         "bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -544,6 +604,11 @@ def bench_multi(args):
         # per peer (the traffic of a reduce-scatter + all-gather)
         per_dir = (world - 1) * (n * 8 // world) * args.steps / t / 1e9
         peak = (world - 1) * XGMI_LINK_GBS
+        agg = args.steps * B / t / 1e9
+        res["hbm_aggregate"] = {"GBs": agg, "peak_GBs": world * HBM_PEAK_GBS,
+                                "frac": agg / (world * HBM_PEAK_GBS),
+                                "note": "(P+1)*nreduce*8 bytes per step over all GPUs vs "
+                                        "P x 8 TB/s; the exchange is xGMI-bound (roofline)"}
         res["roofline"] = {
             "bound": "xgmi", "achieved": per_dir, "peak": peak, "unit": "GB/s",
             "frac": per_dir / peak, "traffic": None,
