@@ -595,15 +595,50 @@ void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned lo
     }
 }
 
-void fused_check(const char *where, const SyncSet &S, unsigned long long epoch, bool word)
+// Device-barrier policy (osgpu_set_device_barrier): wait bound and whether
+// a timed-out call aborts the process (default) or is reported.
+double g_dbar_secs = -1;  // <= 0: OSGPU_DEVICE_BARRIER_TIMEOUT_S, else 10 s
+int g_dbar_fatal = 1;
+
+unsigned long long fused_timeout_ticks(const SyncSet &S)
+{
+    double secs;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        secs = g_dbar_secs;
+    }
+    if (secs <= 0) {
+        const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
+        secs = e ? atof(e) : 10.0;
+        if (secs <= 0) secs = 10.0;
+    }
+    return (unsigned long long) (secs * 1e3 * S.rate_khz);
+}
+
+bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool word)
 {
     const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
+    const bool incomplete = word && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < epoch;
+    if (!err && !incomplete) return true;
+    char msg[256];
     if (err)
-        fatal(where, "device barrier (%s) timed out after %.1f s: a member of the active set "
-                     "did not enter or finish the call",
-              err == 1 ? "entry" : "exit", S.timeout_s);
-    if (word && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < epoch)
-        fatal(where, "fused launch ended without completing epoch %llu", epoch);
+        snprintf(msg, sizeof(msg),
+                 "device barrier (%s) timed out: a member of the active set did not enter or "
+                 "finish the call", err == 1 ? "entry" : "exit");
+    else
+        snprintf(msg, sizeof(msg), "fused launch ended without completing epoch %llu", epoch);
+    int fatal_policy;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        fatal_policy = g_dbar_fatal;
+    }
+    if (fatal_policy) fatal(where, "%s", msg);
+    // reported, not fatal: this call's target is not valid, and the set's
+    // epochs may disagree from now on -- its fused path is switched off
+    set_err("%s: %s", where, msg);
+    __atomic_store_n(S.err_h, 0, __ATOMIC_RELEASE);
+    S.ok = false;
+    return false;
 }
 
 SyncSet *sync_setup(const Coll &c)
@@ -652,10 +687,7 @@ SyncSet *sync_setup(const Coll &c)
     S.max_blocks = std::max(1, cus / (share > 0 ? share : c.PE_size));
     S.peer.resize(peer.size());
     for (size_t i = 0; i < peer.size(); i++) S.peer[i] = (unsigned long long *) peer[i];
-    const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
-    const double secs = e ? atof(e) : 10.0;
-    S.timeout = (unsigned long long) (secs * 1e3 * rate_khz);
-    S.timeout_s = secs;
+    S.rate_khz = rate_khz;
     S.ok = ok;
     return S.ok ? &S : nullptr;
 }
@@ -887,6 +919,14 @@ int osgpu_set_fused_max_bytes(long long bytes)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     g_fused_max = bytes < 0 ? -1 : bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_set_device_barrier(double timeout_s, int fatal_on_timeout)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_dbar_secs = timeout_s;
+    g_dbar_fatal = fatal_on_timeout ? 1 : 0;
     return OSGPU_OK;
 }
 

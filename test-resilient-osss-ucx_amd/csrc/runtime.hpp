@@ -162,8 +162,7 @@ struct SyncSet {
     std::vector<unsigned long long *> peer;    // by active-set index
     std::vector<void *> opened;                // IPC mappings to close
     unsigned long long epoch = 0;
-    unsigned long long timeout = 0;            // wall-clock ticks
-    double timeout_s = 0;
+    int rate_khz = 0;                          // wall clock of the device
     int max_blocks = 0;                        // workgroups per fused launch
     int *err_h = nullptr, *err_d = nullptr;    // host-mapped error word
     unsigned long long *done_h = nullptr, *done_d = nullptr;  // host-mapped completion epoch
@@ -171,7 +170,9 @@ struct SyncSet {
 SyncSet *sync_setup(const Coll &c);
 // wait for a fused launch's completion word (epoch) / report a failed one
 void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned long long epoch);
-void fused_check(const char *where, const SyncSet &S, unsigned long long epoch, bool word);
+// false (not fatal by policy): the call failed, the set's fused path is off
+bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool word);
+unsigned long long fused_timeout_ticks(const SyncSet &S);
 
 // Device view of host memory inside a range pinned with
 // osgpu_host_register, or nullptr.

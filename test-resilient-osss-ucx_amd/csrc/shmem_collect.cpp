@@ -212,7 +212,7 @@ void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg
     a.err = S.err_d;
     a.done_host = S.done_d;
     a.epoch = ++S.epoch;
-    a.timeout = S.timeout;
+    a.timeout = fused_timeout_ticks(S);
     a.P = c.PE_size;
     a.me = S.idx;
     a.max_blocks = S.max_blocks;
@@ -228,7 +228,7 @@ void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg
     } else {
         fused_wait(c.name, S, st, a.epoch);
     }
-    fused_check(c.name, S, a.epoch, !scratch);
+    if (!fused_check(c.name, S, a.epoch, !scratch)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
 }
 
 void run_copy(const CCall &c, const std::vector<const char *> &src, bool counts_done)

@@ -215,7 +215,7 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     a.err = S.err_d;
     a.done_host = S.done_d;
     a.epoch = ++S.epoch;
-    a.timeout = S.timeout;
+    a.timeout = fused_timeout_ticks(S);
     a.n = (size_t) (hi - lo);
     a.P = P;
     a.me = idx;
@@ -257,7 +257,7 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
                 (trace[3] - trace[2]) * tk, (trace[4] - trace[3]) * tk,
                 (trace[6] - trace[5]) * tk);
     }
-    fused_check(c.name, S, a.epoch, !overlap);
+    if (!fused_check(c.name, S, a.epoch, !overlap)) t_last_path = OSGPU_RAN_FUSED_FAILED;
 }
 
 bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *mult)

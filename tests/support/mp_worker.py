@@ -171,6 +171,27 @@ def device_heap_modes(L, PES, mode, rank, world):
         res["digests"], res["paths"] = digests, paths
         if host:
             assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
+    if mode == "timeout":
+        # a member that never enters the call: after one good fused call,
+        # rank 0 calls alone; the device barrier must time out and be
+        # reported (MP_FATAL=0) or abort the process with a message (=1)
+        n = 1024
+        put(0, np.arange(n, dtype=np.int32))
+        torch.cuda.synchronize()
+        sync()
+        L.shmem_int_sum_to_all(dev0 + 8192, dev0, n, 0, 0, world, wrk, psync)
+        res["first"] = osgpu.last_path()
+        sync()
+        fatal = int(os.environ.get("MP_FATAL", "0"))
+        L.osgpu_set_device_barrier(0.5, fatal)
+        if rank == 0:
+            t0 = time.perf_counter()
+            L.shmem_int_sum_to_all(dev0 + 8192, dev0, n, 0, 0, world, wrk, psync)
+            res["alone"] = osgpu.last_path()
+            res["seconds"] = time.perf_counter() - t0
+            res["error"] = L.osgpu_last_error().decode()
+        dist.barrier()
+        L.osgpu_set_device_barrier(-1, 1)
     if mode == "collgolden":
         import hashlib
         from support import coll_cases as CC
@@ -231,7 +252,7 @@ def device_heap_modes(L, PES, mode, rank, world):
         L.osgpu_set_fused_max_bytes(-1)
         L.osgpu_set_path(osgpu.PATH_AUTO)
         res["boundary"] = bound
-    else:  # latency
+    if mode == "latency":
         reps = int(os.environ.get("MP_REPS", "300"))
         lat = {}
         for n in [int(x) for x in os.environ.get("MP_SIZES", "1024,65536,1048576").split(",")]:
@@ -337,7 +358,8 @@ def main():
     counter = [0]
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
-            "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency"):
+            "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
+            "timeout"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -390,7 +412,7 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
-    if mode in ("golden", "goldenhost", "collgolden", "latency"):
+    if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096

@@ -261,3 +261,36 @@ def test_fused_collectives_processes(tmp_path):
                 assert ran == ("copy" if c["kind"] == "collect" else "fused_copy"), (c, r, ran)
                 nfused += ran == "fused_copy"
     assert nfused > 300, nfused
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fatal", [0, 1])
+def test_device_barrier_timeout(tmp_path, monkeypatch, fatal):
+    """A member that never enters a fused call: the others' device barrier
+    gives up after the bound (0.5 s here) -- reported through
+    osgpu_last_error / last_path == fused_failed under the non-fatal policy,
+    an abort with a message under the default fatal one.  Never a hang."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("MP_FATAL", str(fatal))
+    if not fatal:
+        res = launch("timeout", 2, tmp_path)
+        assert res[0]["first"] == "fused_team" and res[1]["first"] == "fused_team"
+        assert res[0]["alone"] == "fused_failed", res[0]
+        assert "device barrier (entry) timed out" in res[0]["error"]
+        assert 0.4 < res[0]["seconds"] < 5.0, res[0]["seconds"]
+        return
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, WORKER, "timeout", str(tmp_path)],
+                                      env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    out0, _ = procs[0].communicate(timeout=120)
+    procs[1].kill()   # waits in dist.barrier for the aborted rank 0
+    procs[1].communicate()
+    assert procs[0].returncode != 0
+    assert "device barrier (entry) timed out" in out0, out0[-2000:]
