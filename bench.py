@@ -26,8 +26,9 @@ N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   / t (SURVEY.md 8d aggregate: sum over GPUs of the shard-fold bytes), t = the
   max over ranks.  Then, in the same run: RCCL allreduce on the same buffers,
   BASELINE config 4 (nreduce = 1 Gi, RCCL) and config 5 (float min/max/prod,
-  128 Mi per PE, host-resident, H2D/D2H included), and fcollect64 over the
-  device heaps (xGMI), RCCL and host staging.  A watchdog prints the line
+  128 Mi per PE, host-resident, H2D/D2H included), fcollect64 over the
+  device heaps (xGMI), RCCL and host staging, and config 1's small call
+  (1 Ki ints) with host barriers vs the fused one-launch path.  A watchdog prints the line
   with what has been measured if the run exceeds --deadline seconds.
 """
 import argparse
@@ -500,6 +501,60 @@ def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_by
     return out
 
 
+def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
+    """BASELINE config 1's shape with one PE per GPU: shmem_int_sum_to_all,
+    nreduce = 1 Ki, device heaps over xGMI -- host barriers vs the fused
+    one-launch path (device-side barriers written across GPUs).  The device
+    barrier is bounded at 2 s and reported instead of fatal here; every rank
+    agrees after each call, so a failure ends the phase cleanly."""
+    n = 1024
+    ps = PES.pes_heap(rank) + (1 << 20) - 4096       # symmetric pSync
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    src = hsrc[:n * 4].view(torch.int32)
+    tgt = htgt[:n * 4].view(torch.int32)
+    src.copy_(torch.arange(n, dtype=torch.int32, device=hsrc.device) + rank)
+    torch.cuda.synchronize()
+    want = world * torch.arange(n, dtype=torch.int32) + world * (world - 1) // 2
+    wrk = (ctypes.c_int * 64)()
+    out = {"note": f"shmem_int_sum_to_all nreduce={n}, one PE per GPU, device heaps; "
+                   f"us = max over ranks of the median call time ({reps} calls)"}
+    L.osgpu_set_path(osgpu.PATH_AUTO)
+    L.osgpu_set_device_barrier(2.0, 0)
+    try:
+        for name, lim in (("host_barriers", 0), ("fused", -1)):
+            L.osgpu_set_fused_max_bytes(lim)
+            ts, paths, failed = [], set(), False
+            for r in range(reps + 10):
+                PES.pes_barrier(0, 0, world, None)
+                t0 = time.perf_counter()
+                L.shmem_int_sum_to_all(tgt.data_ptr(), src.data_ptr(), n, 0, 0, world, wrk, ps)
+                t = time.perf_counter() - t0
+                p = osgpu.last_path()
+                paths.add(p)
+                bad = torch.tensor([1 if p == "fused_failed" else 0])
+                dist.all_reduce(bad)
+                if int(bad.item()):
+                    failed = True
+                    break
+                if r >= 10:
+                    ts.append(t)
+            mine = sorted(ts)[len(ts) // 2] * 1e6 if ts else float("nan")
+            tt = torch.tensor([mine], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ok = (not failed) and bool(torch.equal(tgt.cpu(), want))
+            res = {"us": float(tt.item()), "paths": sorted(paths),
+                   "correct_all_ranks": _agree(dist, world, ok)}
+            if failed:
+                res["error"] = L.osgpu_last_error().decode()
+            out[name] = res
+            if failed:
+                break
+    finally:
+        L.osgpu_set_fused_max_bytes(-1)
+        L.osgpu_set_device_barrier(-1, 1)
+    return out
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -616,6 +671,9 @@ def bench_multi(args):
             "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
                      f"second (it sends as many); peak = {world - 1} x {XGMI_LINK_GBS} GB/s per "
                      f"direction (MI355X xGMI, 153.6 GB/s bidirectional per link)")}
+        if ndev < world:  # a rehearsal with ranks sharing GPUs: no xGMI involved
+            res["roofline"]["frac"] = None
+            res["roofline"]["note"] += "; ranks share a GPU here, so no link is used"
         res["parity_sample"] = _sample_parity(rank, world, src, tgt, n, "sum", dist)
         _log(rank, "team done")
     else:
@@ -712,6 +770,16 @@ def bench_multi(args):
             _log(rank, "collectives done")
         except Exception as e:
             res["collectives"] = {"error": repr(e)[:300]}
+
+    # ---- BASELINE config 1's shape across GPUs: fused one-launch path vs
+    # host barriers
+    if team_ok and not args.no_extra:
+        state["phase"] = "small_calls"
+        try:
+            res["small_calls"] = _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES)
+            _log(rank, "small calls done")
+        except Exception as e:
+            res["small_calls"] = {"error": repr(e)[:300]}
 
     state["phase"] = "teardown"
     emit()
