@@ -501,6 +501,42 @@ def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_by
     return out
 
 
+def _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes, reps=5):
+    """Link characteristics for the next design step: every GPU at once
+    copies one chunk per peer over xGMI with the copy kernel, either PULLING
+    (peer HBM -> my HBM: remote reads) or PUSHING (my HBM -> peer HBM: remote
+    writes into a region only I write).  GB/s per GPU per direction."""
+    chunk = (seg_bytes // world) // 4096 * 4096
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    out = {"chunk_bytes_per_peer": chunk}
+    for name in ("pull_reads", "push_writes"):
+        dsts, srcs, nbs = [], [], []
+        for q in range(world):
+            if q == rank:
+                continue
+            if name == "pull_reads":   # my target block q <- peer q's source block rank
+                srcs.append(bases[(q, 0)] + rank * chunk)
+                dsts.append(bases[(rank, 1)] + q * chunk)
+            else:                      # peer q's target block rank <- my source block q
+                srcs.append(bases[(rank, 0)] + q * chunk)
+                dsts.append(bases[(q, 1)] + rank * chunk)
+            nbs.append(chunk)
+        m = len(nbs)
+        D = (ctypes.c_void_p * m)(*dsts)
+        S = (ctypes.c_void_p * m)(*srcs)
+        N = (ctypes.c_size_t * m)(*nbs)
+
+        def step():
+            assert L.osgpu_copy(D, S, N, m, sp) == 0
+            st.synchronize()
+
+        t = _timed(step, reps, 1, dist, torch)
+        out[name + "_GBs_per_gpu"] = reps * m * chunk / t / 1e9
+        out[name + "_GBs_per_link"] = reps * chunk / t / 1e9
+    return out
+
+
 def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
     """BASELINE config 1's shape with one PE per GPU: shmem_int_sum_to_all,
     nreduce = 1 Ki, device heaps over xGMI -- host barriers vs the fused
@@ -621,6 +657,7 @@ def bench_multi(args):
     # ---- IPC exchange of both segments, agreed on by every rank
     state["phase"] = "ipc"
     mapped = []
+    bases = {}
     ok = seg_bytes < (2 << 30)
     handles = []
     for seg in (hsrc, htgt):
@@ -642,6 +679,7 @@ def bench_multi(args):
                         mapped.append(base)
                 if base:
                     L.osgpu_heap_register_segment(pe, s, ctypes.c_void_p(base), seg_bytes)
+                    bases[(pe, s)] = base
         team_ok = _agree(dist, world, ok)
     _log(rank, f"ipc heaps ready: {team_ok}")
 
@@ -770,6 +808,15 @@ def bench_multi(args):
             _log(rank, "collectives done")
         except Exception as e:
             res["collectives"] = {"error": repr(e)[:300]}
+
+    # ---- link probe: remote reads vs remote writes over xGMI
+    if team_ok and not args.no_extra:
+        state["phase"] = "xgmi_probe"
+        try:
+            res["xgmi_probe"] = _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes)
+            _log(rank, "xgmi probe done")
+        except Exception as e:
+            res["xgmi_probe"] = {"error": repr(e)[:300]}
 
     # ---- BASELINE config 1's shape across GPUs: fused one-launch path vs
     # host barriers
