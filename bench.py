@@ -608,7 +608,9 @@ def bench_multi(args):
     PES = peshm.init(rank, world, 1 << 20, dist, tag="b")
     assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
     n = args.nreduce
-    psync = (ctypes.c_long * 128)()
+    # symmetric pSync (OpenSHMEM requires it; the staging setups of the push
+    # exchange and the host paths publish through it with getmem)
+    psync = ctypes.c_void_p(PES.pes_heap(rank) + (1 << 20) - 8192)
     wrk = (ctypes.c_double * 64)()
     fn = L.shmem_double_sum_to_all
     B = (world + 1) * n * 8          # sum over GPUs of shard-fold bytes
@@ -714,6 +716,26 @@ def bench_multi(args):
             res["roofline"]["note"] += "; ranks share a GPU here, so no link is used"
         res["parity_sample"] = _sample_parity(rank, world, src, tgt, n, "sum", dist)
         _log(rank, "team done")
+        # the push form of the same exchange (remote writes only, staged
+        # through the owners' inboxes): same bytes on the links
+        state["phase"] = "team_push"
+        try:
+            L.osgpu_set_team_exchange(1)
+            tgt.zero_()
+            torch.cuda.synchronize()
+            tp = _timed(step, args.steps, args.warmup, dist, torch)
+            res["team_push"] = {"value": args.steps * B / tp / GIB,
+                                "ms_per_step": tp / args.steps * 1e3,
+                                "algbw_GiBs": n * 8 * args.steps / tp / GIB,
+                                "xgmi_GBs_per_gpu_per_direction":
+                                    (world - 1) * (n * 8 // world) * args.steps / tp / 1e9,
+                                "parity_sample": _sample_parity(rank, world, src, tgt, n, "sum",
+                                                                dist)}
+            _log(rank, "team push done")
+        except Exception as e:
+            res["team_push"] = {"error": repr(e)[:300]}
+        finally:
+            L.osgpu_set_team_exchange(-1)
     else:
         res["team_error"] = "HIP IPC export/import of the device heaps failed on some rank"
 

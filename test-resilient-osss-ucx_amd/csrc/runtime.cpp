@@ -555,6 +555,18 @@ void *host_device_view(const void *p, size_t nbytes)
     return nullptr;
 }
 
+int g_team_exchange = -1;  // -1: from OSGPU_TEAM_EXCHANGE (pull|push), default pull
+
+int team_exchange()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_team_exchange < 0) {
+        const char *e = getenv("OSGPU_TEAM_EXCHANGE");
+        g_team_exchange = (e && !strcmp(e, "push")) ? 1 : 0;
+    }
+    return g_team_exchange;
+}
+
 long long g_fused_max = -1;  // -1: from the environment
 
 size_t fused_max_bytes()
@@ -919,6 +931,14 @@ int osgpu_set_fused_max_bytes(long long bytes)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     g_fused_max = bytes < 0 ? -1 : bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_set_team_exchange(int mode)
+{
+    if (mode < -1 || mode > 1) return OSGPU_EINVAL;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_team_exchange = mode;
     return OSGPU_OK;
 }
 

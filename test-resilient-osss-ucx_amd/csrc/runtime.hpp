@@ -174,6 +174,11 @@ void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned lo
 bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool word);
 unsigned long long fused_timeout_ticks(const SyncSet &S);
 
+// Team exchange form: 0 pull (remote reads, default), 1 push (remote writes
+// through the members' staging inboxes); osgpu_set_team_exchange /
+// OSGPU_TEAM_EXCHANGE.
+int team_exchange();
+
 // Device view of host memory inside a range pinned with
 // osgpu_host_register, or nullptr.
 void *host_device_view(const void *p, size_t nbytes);

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/osgpu_reduce.h"
@@ -135,6 +136,71 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     stream_wait(c.name, st);
     DBG("%s PE %d: team kernel done", c.name, c.me);
     barrier(c);  // src/reductions.c:113 -- every shard of my target is written
+}
+
+// Push form of the team exchange (osgpu_set_team_exchange(1)): every byte
+// crosses the fabric as a remote WRITE.  Per chunk of every shard:
+//   scatter  PE q copies its source's part of shard g into slot q of PE g's
+//            inbox (the STAGED path's IPC-mapped staging, 4 x slot bytes per
+//            PE: P slots of C elements), for every g -- one copy launch;
+//   barrier  every inbox holds the chunk (every member has entered, so every
+//            target is writable);
+//   fold     PE g runs the team kernel over its inbox (local HBM reads) and
+//            writes shard g of every member's target (remote writes);
+//   barrier  every inbox slot is drained / every target shard written.
+// Same fabric bytes as the pull form ((P-1)/P * N * s each way per PE),
+// plus N * s of local inbox traffic; which form the links prefer is
+// measured by bench.py's N > 1 xgmi_probe.
+void run_team_push(const Call &c, const std::vector<const void *> &srcs,
+                   const std::vector<void *> &dsts, int idx, StageSet &S)
+{
+    hipStream_t st = pe_stream(c.name, c.me);
+    const size_t s = type_size(c.type);
+    const int P = c.PE_size;
+    const long long g16 = s >= 16 ? 1 : (long long) (16 / s);
+    std::vector<long long> lo(P), hi(P);
+    long long most = 0;
+    for (int g = 0; g < P; g++) {
+        osgpu_shard_range(c.nreduce, P, g, (int) (s > 16 ? 16 : s), &lo[g], &hi[g]);
+        most = std::max(most, hi[g] - lo[g]);
+    }
+    long long C = (long long) ((4 * S.slot) / (size_t) P / s) / g16 * g16;  // elements per slot
+    if (C < 1) fatal(c.name, "staging too small for the push exchange of %d PEs", P);
+    const long long nchunks = (most + C - 1) / C;
+    t_last_path = OSGPU_RAN_TEAM_PUSH;
+    DBG("%s PE %d: team push, %lld chunks of %lld", c.name, c.me, nchunks, C);
+    entry_sync(c.name, st);
+    std::vector<osgpu::CopySeg> segs;
+    std::vector<const void *> sp(P);
+    std::vector<void *> dp(P);
+    for (long long k = 0; k < nchunks; k++) {
+        segs.clear();
+        for (int g = 0; g < P; g++) {
+            const long long a = lo[g] + k * C, b = std::min(hi[g], a + C);
+            if (b > a)
+                segs.push_back({(const char *) srcs[idx] + (size_t) a * s,
+                                S.region(g) + (size_t) idx * C * s, (size_t) (b - a) * s});
+        }
+        for (size_t i = 0; i < segs.size(); i += osgpu::kMaxCopySegs) {
+            const int m = (int) std::min(segs.size() - i, (size_t) osgpu::kMaxCopySegs);
+            hipError_t e = osgpu::launch_copy(segs.data() + i, m, st);
+            if (e != hipSuccess) fatal(c.name, "scatter launch: %s", hipGetErrorString(e));
+        }
+        stream_wait(c.name, st);
+        barrier(c);  // every inbox holds chunk k; every member has entered (:82)
+        const long long a = lo[idx] + k * C, b = std::min(hi[idx], a + C);
+        if (b > a) {
+            for (int i = 0; i < P; i++) {
+                sp[i] = S.region(idx) + (size_t) i * C * s;
+                dp[i] = (char *) dsts[i] + (size_t) a * s;
+            }
+            hipError_t e = osgpu::launch_team(c.type, c.op, P, dp.data(), sp.data(),
+                                              (size_t) (b - a), st);
+            if (e != hipSuccess) fatal(c.name, "team fold launch: %s", hipGetErrorString(e));
+            stream_wait(c.name, st);
+        }
+        barrier(c);  // inboxes drained; after the last chunk every target is complete (:113)
+    }
 }
 
 void run_p2p(const Call &c, const std::vector<const void *> &srcs)
@@ -510,8 +576,11 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     SyncSet *S = nullptr;
     if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_P2P) &&
         (idx = team_ptrs(c, srcs, dsts)) >= 0) {
+        StageSet *G = nullptr;
         if (fused_eligible(c, true) && (S = sync_setup(c)))
             run_fused(c, *S, srcs, dsts, true);
+        else if (team_exchange() == 1 && c.ops.getmem && (G = stage_setup(c)))
+            run_team_push(c, srcs, dsts, idx, *G);
         else
             run_team(c, srcs, dsts, idx);
     } else if (mode != OSGPU_PATH_RCCL && member_sources(c, srcs)) {

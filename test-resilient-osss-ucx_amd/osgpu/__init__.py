@@ -32,7 +32,7 @@ CTYPE = {
 PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
 # enum osgpu_ran: what osgpu_last_path() reports
 RAN = ["none", "team", "pull", "rccl", "staged", "getmem", "fused_team", "fused_pull",
-       "barrier_only", "fused_staged", "copy", "fused_copy", "fused_failed"]
+       "barrier_only", "fused_staged", "copy", "fused_copy", "fused_failed", "team_push"]
 
 
 def has_op(t: str, op: str) -> bool:
@@ -135,6 +135,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_host_unregister.argtypes = [vp]
     L.osgpu_set_fused_max_bytes.argtypes = [ctypes.c_longlong]
     L.osgpu_set_device_barrier.argtypes = [ctypes.c_double, ctypes.c_int]
+    L.osgpu_set_team_exchange.argtypes = [ctypes.c_int]
     L.osgpu_last_path.restype = ctypes.c_int
     L.osgpu_last_coll_path.restype = ctypes.c_int
     L.osgpu_last_error.restype = ctypes.c_char_p

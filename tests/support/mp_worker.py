@@ -466,11 +466,13 @@ def main():
             # runtime has getmem for the flag-area exchange), 0 = host barriers
             for path, inplace, fused in ((osgpu.PATH_AUTO, False, -1), (osgpu.PATH_AUTO, False, 0),
                                          (osgpu.PATH_PULL, False, -1), (osgpu.PATH_PULL, False, 0),
-                                         (osgpu.PATH_AUTO, True, -1)):
+                                         (osgpu.PATH_AUTO, True, -1), (osgpu.PATH_AUTO, False, 9)):
+                # fused 9: host barriers with the push form of the team exchange
+                L.osgpu_set_team_exchange(1 if fused == 9 else 0)
                 heap[: raw.size].copy_(torch.from_numpy(raw.copy()).cuda())
                 torch.cuda.synchronize()
                 L.osgpu_set_path(path)
-                L.osgpu_set_fused_max_bytes(fused)
+                L.osgpu_set_fused_max_bytes(0 if fused == 9 else fused)
                 # pSync must be symmetric (getmem-able) when the runtime has getmem
                 psync = (PES.pes_heap(rank) + (1 << 24) - 8192 if PES is not None
                          else ctypes.addressof((ctypes.c_long * 128)()))
@@ -489,6 +491,7 @@ def main():
                 dist.barrier()
         L.osgpu_set_path(osgpu.PATH_AUTO)
         L.osgpu_set_fused_max_bytes(-1)
+        L.osgpu_set_team_exchange(-1)
         if PES is not None:  # collect needs the runtime's getmem (pSync words)
             psync = PES.pes_heap(rank) + (1 << 24) - 4096
 

@@ -11,6 +11,7 @@ ragged/misaligned spans and the raw combine launcher are checked against the
 oracle on the same inputs.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -105,6 +106,29 @@ def test_device_resident_matches_golden(torch_cuda, pair, cases):
         act = O.active_set(c["PE_start"], c["logPE_stride"], c["PE_size"])
         want = _expected_path(c, True)
         assert all(tm.last_paths[pe] == want for pe in act), (tm.last_paths, want)
+
+
+def test_team_push_matches_golden(torch_cuda):
+    """Every golden case through the push form of the team exchange
+    (osgpu_set_team_exchange(1)): sources scattered into the owners'
+    staging inboxes, folded there, results written to every target -- the
+    fabric sees remote writes only.  Small staging slots force many chunks."""
+    tm = team(device=True)
+    L = tm.lib
+    L.osgpu_finalize()
+    os.environ["OSGPU_STAGE_BYTES"] = "65536"
+    L.osgpu_set_team_exchange(1)
+    try:
+        for c in CASES:
+            check(c, run_case(tm, c))
+            act = O.active_set(c["PE_start"], c["logPE_stride"], c["PE_size"])
+            want = ("barrier_only" if c["nreduce"] == 0 else
+                    "team_push" if c["PE_size"] >= 2 else "pull")
+            assert all(tm.last_paths[pe] == want for pe in act), (tm.last_paths, want)
+    finally:
+        L.osgpu_set_team_exchange(-1)
+        L.osgpu_finalize()
+        del os.environ["OSGPU_STAGE_BYTES"]
 
 
 def test_pull_path_matches_golden(torch_cuda):

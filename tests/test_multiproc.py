@@ -124,6 +124,8 @@ def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
                 fusable = (pes == "shm" and fused == "-1" and t != "longdouble" and
                            n * s <= (1 << 20) // (1 if team else 4))
                 want = ("fused_" if fusable else "") + ("team" if team else "pull")
+                if fused == "9":  # push form: needs the staging exchange (getmem)
+                    want = "team_push" if pes == "shm" else "team"
                 assert ran == want, (key, r, ran)
     if pes == "shm":  # collect needs getmem: the shm runtime has it
         _check_colls(res, "device")
