@@ -69,7 +69,8 @@ def expected(kind, bits, counts, root, world):
 # expected target region (margins included) from oracle_coll.
 
 MARGIN = 256
-FUSED_SETS = [(2, 0, 0, 2), (3, 0, 0, 3), (4, 0, 0, 4), (4, 1, 0, 3), (4, 0, 1, 2)]
+FUSED_SETS = [(2, 0, 0, 2), (3, 0, 0, 3), (4, 0, 0, 4), (4, 1, 0, 3), (4, 0, 1, 2),
+              (8, 0, 0, 8), (8, 1, 1, 3), (8, 2, 0, 6)]
 
 
 def _align(x, a=256):
