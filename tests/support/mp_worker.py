@@ -170,6 +170,28 @@ def device_heap_modes(L, PES, mode, rank, world):
         L.osgpu_set_path(osgpu.PATH_AUTO)
         res["digests"], res["paths"] = digests, paths
         if host:
+            # misaligned host arrays: the kernel's PCIe copies fall back to
+            # dword / byte accesses
+            mis = {}
+            for t, op, so, to in (("int", "sum", 4, 4), ("short", "prod", 2, 6),
+                                  ("double", "sum", 8, 12), ("complexf", "prod", 3, 5)):
+                s = np.dtype(O.NP_DTYPE[t]).itemsize
+                for n in (1, 1000, 4099):
+                    src = O.team_inputs(t, world, n, 0x77 + n, "wide")
+                    want = O.to_all(t, op, src)[rank]
+                    raw = np.ascontiguousarray(src[rank]).view(np.uint8).reshape(-1)
+                    toff = (n * s + 8192 + 4095) // 4096 * 4096 + to
+                    ctypes.memmove(hbase + so, raw.ctypes.data, raw.size)
+                    ctypes.memset(hbase + toff, 0x5A, n * s)
+                    sync()
+                    getattr(L, f"shmem_{t}_{op}_to_all")(hbase + toff, hbase + so, n, 0, 0,
+                                                         world, wrk, psync)
+                    got = np.frombuffer(ctypes.string_at(hbase + toff, n * s), np.uint8)
+                    mis[f"{t}/{op}/{n}/{so}/{to}"] = [
+                        bool(np.array_equal(got, want.view(np.uint8).reshape(-1))),
+                        osgpu.last_path()]
+                    sync()
+            res["misaligned"] = mis
             assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
     if mode == "timeout":
         # a member that never enters the call: after one good fused call,
@@ -252,6 +274,34 @@ def device_heap_modes(L, PES, mode, rank, world):
         L.osgpu_set_fused_max_bytes(-1)
         L.osgpu_set_path(osgpu.PATH_AUTO)
         res["boundary"] = bound
+        # misaligned arrays: a shared 16-B phase (vector body + scalar head
+        # and tail edges) and differing phases (element-wise body)
+        mis = {}
+        for t, op in (("short", "sum"), ("int", "prod"), ("float", "sum"), ("double", "prod"),
+                      ("complexf", "sum"), ("complexd", "prod"), ("long", "xor")):
+            s = np.dtype(O.NP_DTYPE[t]).itemsize
+            for n in (1, 17, 1000, 4099):
+                src = O.team_inputs(t, world, n, 0x99 + n, "wide" if t != "long" else "bits")
+                want = O.to_all(t, op, src)[rank]
+                for so, to in ((s, s), (s, 2 * s), (0, s), (8, 8)):
+                    if so % s or to % s:
+                        continue
+                    toff = (n * s + 8192 + 4095) // 4096 * 4096 + to
+                    for path in (osgpu.PATH_AUTO, osgpu.PATH_PULL):
+                        L.osgpu_set_path(path)
+                        put(so, src[rank])
+                        heap[toff:toff + n * s].fill_(0x5A)
+                        torch.cuda.synchronize()
+                        sync()
+                        getattr(L, f"shmem_{t}_{op}_to_all")(dev0 + toff, dev0 + so, n, 0, 0,
+                                                             world, wrk, psync)
+                        got = heap[toff:toff + n * s].cpu().numpy()
+                        mis[f"{t}/{op}/{n}/{so}/{to}/{path}"] = [
+                            bool(np.array_equal(got, want.view(np.uint8).reshape(-1))),
+                            osgpu.last_path()]
+                        sync()
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        res["misaligned"] = mis
     if mode == "latency":
         reps = int(os.environ.get("MP_REPS", "300"))
         lat = {}

@@ -201,6 +201,12 @@ def test_fused_path_golden_processes(tmp_path):
         for key, (exact, ran, fused) in res[r]["boundary"].items():
             assert exact, (key, r)
             assert ran.startswith("fused_") == fused, (key, r, ran)
+    # misaligned sources/targets (shared and differing 16-B phases), fused
+    for r in range(world):
+        assert len(res[r]["misaligned"]) > 100
+        for key, (exact, ran) in res[r]["misaligned"].items():
+            assert exact, (key, r)
+            assert ran.startswith("fused_"), (key, r, ran)
 
 
 @pytest.mark.gpu
@@ -235,6 +241,9 @@ def test_fused_staged_golden_processes(tmp_path):
             assert ran == want, (key, r, ran, want)
             nfused += ran == "fused_staged"
     assert nchecked > 1000 and nfused > 700, (nchecked, nfused)
+    for r in range(world):  # misaligned host arrays (dword / byte PCIe copies)
+        for key, (exact, ran) in res[r]["misaligned"].items():
+            assert exact and ran == "fused_staged", (key, r, ran)
 
 
 @pytest.mark.gpu
