@@ -92,6 +92,18 @@ bool fused_supported(int type);
 hipError_t launch_fused_copy(const FusedArgs &a, hipStream_t s);
 hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s);
 
+// Full-size parity checks on the GPU (verify.hip).  Checksum of n elements
+// of elem_bytes (2, 4, 8, 16) into *out (device memory, zeroed by the
+// caller): CK_SUM adds the zero-extended elements mod 2^64, CK_XOR xors
+// them, CK_HASH adds a position-weighted mix of each element's bits.
+// Compare: out[0] += differing 16-B vectors (bytes when unaligned), out[1]
+// = min(out[1], byte offset of the first difference); out[1] preset to ~0.
+enum { CK_SUM = 0, CK_XOR = 1, CK_HASH = 2 };
+hipError_t launch_checksum(int elem_bytes, int mode, const void *p, size_t n,
+                           unsigned long long *out, hipStream_t s);
+hipError_t launch_compare(const void *a, const void *b, size_t nbytes, unsigned long long *out,
+                          hipStream_t s);
+
 // x87 80-bit extended combine (soft-float on the GPU), longdouble.hip
 hipError_t launch_longdouble(int op, void *out, const void *const *srcs, int k, size_t n,
                              hipStream_t s);

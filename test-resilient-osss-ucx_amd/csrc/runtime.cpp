@@ -514,6 +514,26 @@ bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &
     return all_ok;
 }
 
+// One H2D and one D2H stream per device for every PE of this process: the
+// DMA engines run one copy per direction at full duplex (48.6 GB/s each way
+// on this link), but two per direction at once drop to 28.7 GB/s each way
+// (tools/pcie_kernel_probe.hip, profiles/r01_pcie_kernel_probe.jsonl), so
+// PEs that are threads of one process queue their staging copies on the
+// same pair instead of competing.
+std::map<int, std::pair<hipStream_t, hipStream_t>> g_copy_streams;
+
+void device_copy_streams(const char *where, int dev, hipStream_t *in, hipStream_t *out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto &p = g_copy_streams[dev];
+    if (!p.first) {
+        HIPCHK(where, hipStreamCreateWithFlags(&p.first, hipStreamNonBlocking));
+        HIPCHK(where, hipStreamCreateWithFlags(&p.second, hipStreamNonBlocking));
+    }
+    *in = p.first;
+    *out = p.second;
+}
+
 StageSet *stage_setup(const Coll &c)
 {
     int dev = 0;
@@ -527,9 +547,8 @@ StageSet *stage_setup(const Coll &c)
     S.device = dev;
     S.slot = stage_slot_bytes();
     HIPCHK(c.name, hipMalloc((void **) &S.local, 4 * S.slot));
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_in, hipStreamNonBlocking));
+    device_copy_streams(c.name, dev, &S.st_in, &S.st_out);
     HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_c, hipStreamNonBlocking));
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_out, hipStreamNonBlocking));
     for (int s = 0; s < 2; s++) {
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_in[s], hipEventDisableTiming));
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_out[s], hipEventDisableTiming));
@@ -860,11 +879,14 @@ int osgpu_finalize(void)
             if (S.ev_in[s]) (void) hipEventDestroy(S.ev_in[s]);
             if (S.ev_out[s]) (void) hipEventDestroy(S.ev_out[s]);
         }
-        if (S.st_in) (void) hipStreamDestroy(S.st_in);
         if (S.st_c) (void) hipStreamDestroy(S.st_c);
-        if (S.st_out) (void) hipStreamDestroy(S.st_out);
     }
     g_stage.clear();
+    for (auto &kv : g_copy_streams) {  // shared by the staging sets above
+        if (kv.second.first) (void) hipStreamDestroy(kv.second.first);
+        if (kv.second.second) (void) hipStreamDestroy(kv.second.second);
+    }
+    g_copy_streams.clear();
     for (auto &kv : g_sync) {
         SyncSet &S = kv.second;
         for (void *p : S.opened) (void) hipIpcCloseMemHandle(p);
@@ -1001,6 +1023,85 @@ int osgpu_copy(void *const *dsts, const void *const *srcs, const size_t *bytes, 
             return OSGPU_EHIP;
         }
     }
+    return OSGPU_OK;
+}
+
+// result words of the verification launchers, per thread and device
+struct VerifyBuf {
+    int device = -1;
+    unsigned long long *d = nullptr, *h = nullptr;
+};
+thread_local VerifyBuf t_vbuf;
+
+static int verify_begin(const char *where, void *hip_stream, hipStream_t *st)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_err("%s: no GPU", where);
+        return OSGPU_EHIP;
+    }
+    if (!t_vbuf.d || t_vbuf.device != dev) {
+        if (hipMalloc((void **) &t_vbuf.d, 2 * sizeof(unsigned long long)) != hipSuccess ||
+            hipHostMalloc((void **) &t_vbuf.h, 2 * sizeof(unsigned long long),
+                          hipHostMallocDefault) != hipSuccess) {
+            set_err("%s: out of memory", where);
+            return OSGPU_EHIP;
+        }
+        t_vbuf.device = dev;
+    }
+    *st = hip_stream ? (hipStream_t) hip_stream : thread_stream(where);
+    return OSGPU_OK;
+}
+
+static int verify_end(const char *where, hipError_t e, hipStream_t st)
+{
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(t_vbuf.h, t_vbuf.d, 2 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        set_err("%s: %s", where, hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
+int osgpu_checksum(int type, int mode, const void *data, size_t nelems, void *hip_stream,
+                   unsigned long long *result)
+{
+    const size_t es = type_size(type);
+    if (!es || mode < 0 || mode > 2 || !result || (!data && nelems)) {
+        set_err("osgpu_checksum: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    hipStream_t st;
+    int rc = verify_begin("osgpu_checksum", hip_stream, &st);
+    if (rc) return rc;
+    hipError_t e = hipMemsetAsync(t_vbuf.d, 0, 2 * sizeof(unsigned long long), st);
+    if (e == hipSuccess && nelems)
+        e = osgpu::launch_checksum((int) es, mode, data, nelems, t_vbuf.d, st);
+    if ((rc = verify_end("osgpu_checksum", e, st))) return rc;
+    *result = t_vbuf.h[0];
+    return OSGPU_OK;
+}
+
+int osgpu_compare(const void *a, const void *b, size_t nbytes, void *hip_stream,
+                  unsigned long long *mismatches, unsigned long long *first_offset)
+{
+    if (!mismatches || (nbytes && (!a || !b))) {
+        set_err("osgpu_compare: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    hipStream_t st;
+    int rc = verify_begin("osgpu_compare", hip_stream, &st);
+    if (rc) return rc;
+    hipError_t e = hipMemsetAsync(t_vbuf.d, 0, sizeof(unsigned long long), st);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(t_vbuf.d + 1, 0xff, sizeof(unsigned long long), st);
+    if (e == hipSuccess && nbytes) e = osgpu::launch_compare(a, b, nbytes, t_vbuf.d, st);
+    if ((rc = verify_end("osgpu_compare", e, st))) return rc;
+    *mismatches = t_vbuf.h[0];
+    if (first_offset) *first_offset = t_vbuf.h[1];
     return OSGPU_OK;
 }
 

@@ -136,12 +136,36 @@ def load() -> ctypes.CDLL:
     L.osgpu_set_fused_max_bytes.argtypes = [ctypes.c_longlong]
     L.osgpu_set_device_barrier.argtypes = [ctypes.c_double, ctypes.c_int]
     L.osgpu_set_team_exchange.argtypes = [ctypes.c_int]
+    L.osgpu_checksum.argtypes = [i, i, vp, sz, vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.osgpu_compare.argtypes = [vp, vp, sz, vp, ctypes.POINTER(ctypes.c_ulonglong),
+                                ctypes.POINTER(ctypes.c_ulonglong)]
     L.osgpu_last_path.restype = ctypes.c_int
     L.osgpu_last_coll_path.restype = ctypes.c_int
     L.osgpu_last_error.restype = ctypes.c_char_p
     L.osgpu_version.restype = ctypes.c_char_p
     _LIB = L
     return L
+
+
+CK_SUM, CK_XOR, CK_HASH = 0, 1, 2
+
+
+def checksum(t: str, mode: int, ptr: int, n: int, stream: int | None = None) -> int:
+    """osgpu_checksum over n elements of type t at device address ptr."""
+    out = ctypes.c_ulonglong()
+    rc = load().osgpu_checksum(TYPES.index(t), mode, ptr, n, stream, ctypes.byref(out))
+    if rc != 0:
+        raise RuntimeError(load().osgpu_last_error().decode())
+    return out.value
+
+
+def compare(a: int, b: int, nbytes: int, stream: int | None = None):
+    """osgpu_compare: (differing 16-B vectors, first differing byte offset or None)."""
+    bad, first = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    rc = load().osgpu_compare(a, b, nbytes, stream, ctypes.byref(bad), ctypes.byref(first))
+    if rc != 0:
+        raise RuntimeError(load().osgpu_last_error().decode())
+    return bad.value, (None if first.value == (1 << 64) - 1 else first.value)
 
 
 def last_path() -> str:
