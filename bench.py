@@ -720,17 +720,23 @@ def bench_multi(args):
         # through the owners' inboxes): same bytes on the links
         state["phase"] = "team_push"
         try:
+            # full-size identity of the two exchange forms: a position-weighted
+            # hash of every PE's whole target (verify.hip), before and after
+            h_pull = osgpu.checksum("double", osgpu.CK_HASH, tgt.data_ptr(), n)
             L.osgpu_set_team_exchange(1)
             tgt.zero_()
             torch.cuda.synchronize()
             tp = _timed(step, args.steps, args.warmup, dist, torch)
+            h_push = osgpu.checksum("double", osgpu.CK_HASH, tgt.data_ptr(), n)
             res["team_push"] = {"value": args.steps * B / tp / GIB,
                                 "ms_per_step": tp / args.steps * 1e3,
                                 "algbw_GiBs": n * 8 * args.steps / tp / GIB,
                                 "xgmi_GBs_per_gpu_per_direction":
                                     (world - 1) * (n * 8 // world) * args.steps / tp / 1e9,
                                 "parity_sample": _sample_parity(rank, world, src, tgt, n, "sum",
-                                                                dist)}
+                                                                dist),
+                                "full_target_identical_to_pull_all_ranks":
+                                    _agree(dist, world, h_pull == h_push)}
             _log(rank, "team push done")
         except Exception as e:
             res["team_push"] = {"error": repr(e)[:300]}
