@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "../../include/osgpu_reduce.h"
@@ -380,6 +381,46 @@ void run_rccl(const Call &c)
     }
 }
 
+// Pageable host arrays: the runtime's own bounce copies move ~27 GB/s each
+// way; this path stages them through the PE's pinned bounce slots with a
+// multi-threaded memcpy instead (OSGPU_COPY_THREADS, default 4), so the DMA
+// always runs from pinned memory.
+bool host_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void) hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+void par_memcpy(void *dst, const void *src, size_t n)
+{
+    static const int nt = [] {
+        const char *e = getenv("OSGPU_COPY_THREADS");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : (v > 32 ? 32 : v);
+    }();
+    const size_t min_piece = (size_t) 1 << 20;
+    int k = (int) std::min<size_t>((size_t) nt, (n + min_piece - 1) / min_piece);
+    if (k <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t piece = (n / k + 4095) & ~(size_t) 4095;
+    std::vector<std::thread> th;
+    for (int i = 1; i < k; i++) {
+        const size_t lo = (size_t) i * piece;
+        if (lo >= n) break;
+        const size_t len = std::min(piece, n - lo);
+        th.emplace_back([=] { memcpy((char *) dst + lo, (const char *) src + lo, len); });
+    }
+    memcpy(dst, src, std::min(piece, n));
+    for (auto &t : th) t.join();
+}
+
 void run_staged(const Call &c, StageSet &S)
 {
     const size_t s = type_size(c.type);
@@ -397,11 +438,27 @@ void run_staged(const Call &c, StageSet &S)
     const char *src = (const char *) c.source;
     std::vector<const void *> sp(P);
     std::vector<void *> dp(P);
+    // pinned bounce slots for pageable arrays: in[2], out[2] of S.slot bytes
+    const bool bounce_in = !host_pinned(c.source), bounce_out = !host_pinned(result);
+    char *bounce = (bounce_in || bounce_out)
+                       ? (char *) host_stage(c.name, c.me, 4 * S.slot) : nullptr;
+    auto bin = [&](int sl) { return bounce + (size_t) sl * S.slot; };
+    auto bout = [&](int sl) { return bounce + (size_t) (2 + sl) * S.slot; };
+    auto chunk_n = [&](size_t ch) { return (ch + 1) * C <= N ? C : N - ch * C; };
+    // D2H of chunk ch landed in bout: copy it to the caller's array
+    auto drain = [&](size_t ch) {
+        if (bounce_out) par_memcpy(result + ch * C * s, bout((int) (ch & 1)), chunk_n(ch) * s);
+    };
 
     auto h2d = [&](size_t ch) {
-        const size_t n = (ch + 1) * C <= N ? C : N - ch * C;
-        HIPCHK(c.name, hipMemcpyAsync(S.in(idx, ch & 1), src + ch * C * s, n * s,
-                                      hipMemcpyHostToDevice, S.st_in));
+        const size_t n = chunk_n(ch);
+        const char *from = src + ch * C * s;
+        if (bounce_in) {  // bin[ch & 1] is free: its previous H2D was waited for
+            par_memcpy(bin((int) (ch & 1)), from, n * s);
+            from = bin((int) (ch & 1));
+        }
+        HIPCHK(c.name, hipMemcpyAsync(S.in(idx, ch & 1), from, n * s, hipMemcpyHostToDevice,
+                                      S.st_in));
         HIPCHK(c.name, hipEventRecord(S.ev_in[ch & 1], S.st_in));
     };
     entry_sync(c.name);
@@ -411,7 +468,10 @@ void run_staged(const Call &c, StageSet &S)
         const size_t n = (ch + 1) * C <= N ? C : N - ch * C;
         if (ch + 1 < nchunks) h2d(ch + 1);   // slot reuse is safe: team(ch-1) ended everywhere
         HIPCHK(c.name, hipEventSynchronize(S.ev_in[sl]));
-        if (ch >= 2) HIPCHK(c.name, hipEventSynchronize(S.ev_out[sl]));  // my out slot drained
+        if (ch >= 2) {  // my out slot (and its bounce) drained
+            HIPCHK(c.name, hipEventSynchronize(S.ev_out[sl]));
+            drain(ch - 2);
+        }
         barrier(c);  // chunk ch staged on every PE, every out[sl] free
         if (P == 1) {
             const void *one = S.in(0, sl);
@@ -439,11 +499,12 @@ void run_staged(const Call &c, StageSet &S)
         }
         stream_wait(c.name, S.st_c);
         barrier(c);  // every shard of my out[sl] written
-        HIPCHK(c.name, hipMemcpyAsync(result + ch * C * s, S.out(idx, sl), n * s,
-                                      hipMemcpyDeviceToHost, S.st_out));
+        HIPCHK(c.name, hipMemcpyAsync(bounce_out ? bout(sl) : result + ch * C * s,
+                                      S.out(idx, sl), n * s, hipMemcpyDeviceToHost, S.st_out));
         HIPCHK(c.name, hipEventRecord(S.ev_out[sl], S.st_out));
     }
     stream_wait(c.name, S.st_out);
+    for (size_t ch = nchunks >= 2 ? nchunks - 2 : 0; ch < nchunks; ch++) drain(ch);
     if (overlap) {
         memcpy(c.target, result, c.nbytes);
         free(result);
