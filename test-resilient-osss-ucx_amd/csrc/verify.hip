@@ -69,6 +69,30 @@ __device__ __forceinline__ void block_publish(uint64_t acc, unsigned long long *
     }
 }
 
+// fold the W = 16 / ES elements of vector j
+template <int ES, int MODE>
+__device__ __forceinline__ uint64_t fold_vec(uint64_t acc, u32x4 v, size_t j)
+{
+    if (ES == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            acc = fold_elem<MODE>(acc, v[k] & 0xffffu, j * 8 + 2 * k);
+            acc = fold_elem<MODE>(acc, v[k] >> 16, j * 8 + 2 * k + 1);
+        }
+    } else if (ES == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc = fold_elem<MODE>(acc, v[k], j * 4 + k);
+    } else if (ES == 8) {
+        acc = fold_elem<MODE>(acc, (uint64_t) v[0] | (uint64_t) v[1] << 32, j * 2);
+        acc = fold_elem<MODE>(acc, (uint64_t) v[2] | (uint64_t) v[3] << 32, j * 2 + 1);
+    } else {
+        const uint64_t lo = (uint64_t) v[0] | (uint64_t) v[1] << 32;
+        const uint64_t hi = (uint64_t) v[2] | (uint64_t) v[3] << 32;
+        acc = fold_elem<MODE>(acc, lo ^ mix64(hi), j);
+    }
+    return acc;
+}
+
 // ES: element bytes.  Elements are read 16 B at a time when the array is
 // 16-B aligned (the body), byte-assembled otherwise and for the tail.
 template <int ES, int MODE>
@@ -81,26 +105,21 @@ __global__ __launch_bounds__(kVBlock) void checksum_kernel(const unsigned char *
     uint64_t acc = 0;
     const bool vec = ((uintptr_t) p & 15) == 0;
     const size_t nvec = vec ? n / W : 0;
-    for (size_t j = tid; j < nvec; j += stride) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p) + j);
-        if (ES == 2) {
+    // tiles of kVBlock * 4 consecutive vectors per workgroup, four vectors
+    // in flight per lane; the last partial tile one vector at a time
+    const u32x4 *vp = reinterpret_cast<const u32x4 *>(p);
+    constexpr size_t kTile = (size_t) kVBlock * 4;
+    const size_t full = nvec / kTile;
+    for (size_t t = blockIdx.x; t < full; t += gridDim.x) {
+        const size_t j0 = t * kTile + threadIdx.x;
+        u32x4 w[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                acc = fold_elem<MODE>(acc, v[k] & 0xffffu, j * 8 + 2 * k);
-                acc = fold_elem<MODE>(acc, v[k] >> 16, j * 8 + 2 * k + 1);
-            }
-        } else if (ES == 4) {
+        for (int u = 0; u < 4; u++) w[u] = __builtin_nontemporal_load(vp + j0 + u * kVBlock);
 #pragma unroll
-            for (int k = 0; k < 4; k++) acc = fold_elem<MODE>(acc, v[k], j * 4 + k);
-        } else if (ES == 8) {
-            acc = fold_elem<MODE>(acc, (uint64_t) v[0] | (uint64_t) v[1] << 32, j * 2);
-            acc = fold_elem<MODE>(acc, (uint64_t) v[2] | (uint64_t) v[3] << 32, j * 2 + 1);
-        } else {
-            const uint64_t lo = (uint64_t) v[0] | (uint64_t) v[1] << 32;
-            const uint64_t hi = (uint64_t) v[2] | (uint64_t) v[3] << 32;
-            acc = fold_elem<MODE>(acc, lo ^ mix64(hi), j);
-        }
+        for (int u = 0; u < 4; u++) acc = fold_vec<ES, MODE>(acc, w[u], j0 + u * kVBlock);
     }
+    for (size_t j = full * kTile + tid; j < nvec; j += stride)
+        acc = fold_vec<ES, MODE>(acc, __builtin_nontemporal_load(vp + j), j);
     for (size_t i = nvec * W + tid; i < n; i += stride) {
         const unsigned char *e = p + i * ES;
         uint64_t v = 0;
@@ -128,14 +147,25 @@ __global__ __launch_bounds__(kVBlock) void compare_kernel(const unsigned char *a
     const bool vec = (((uintptr_t) a | (uintptr_t) b) & 15) == 0;
     const size_t nvec = vec ? nbytes / 16 : 0;
     uint64_t bad = 0, first = ~0ull;
-    for (size_t j = tid; j < nvec; j += stride) {
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a) + j);
-        const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(b) + j);
+    auto check = [&](const u32x4 &x, const u32x4 &y, size_t j) {
         const bool diff = x[0] != y[0] || x[1] != y[1] || x[2] != y[2] || x[3] != y[3];
         const uint64_t m = __ballot(diff);  // the wave's differing vectors
         if ((threadIdx.x & 63) == 0) bad += (uint64_t) __popcll(m);
         if (diff && j * 16 < first) first = j * 16;
+    };
+    const u32x4 *va = reinterpret_cast<const u32x4 *>(a), *vb = reinterpret_cast<const u32x4 *>(b);
+    constexpr size_t kTile = (size_t) kVBlock * 2;  // two vectors of each array in flight
+    const size_t full = nvec / kTile;
+    for (size_t t = blockIdx.x; t < full; t += gridDim.x) {
+        const size_t j0 = t * kTile + threadIdx.x;
+        const u32x4 x0 = __builtin_nontemporal_load(va + j0), y0 = __builtin_nontemporal_load(vb + j0);
+        const u32x4 x1 = __builtin_nontemporal_load(va + j0 + kVBlock);
+        const u32x4 y1 = __builtin_nontemporal_load(vb + j0 + kVBlock);
+        check(x0, y0, j0);
+        check(x1, y1, j0 + kVBlock);
     }
+    for (size_t j = full * kTile + tid; j < nvec; j += stride)
+        check(__builtin_nontemporal_load(va + j), __builtin_nontemporal_load(vb + j), j);
     for (size_t i = nvec * 16 + tid; i < nbytes; i += stride)
         if (a[i] != b[i]) {
             bad++;

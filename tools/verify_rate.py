@@ -29,4 +29,17 @@ for name, fn, bytes_ in (
         ts.append(time.perf_counter() - t0)
     t = sorted(ts)[len(ts) // 2]
     out[name] = {"ms": t * 1e3, "GBs": bytes_ / t / 1e9, "frac_of_8TBs": bytes_ / t / 8e12}
+# kernel-only: an empty call's fixed cost (memset + launch + read-back + sync)
+e = torch.empty(16, dtype=torch.int64, device="cuda")
+ts = []
+for _ in range(20):
+    t0 = time.perf_counter()
+    osgpu.checksum("long", osgpu.CK_SUM, e.data_ptr(), 1)
+    ts.append(time.perf_counter() - t0)
+fixed = sorted(ts)[len(ts) // 2]
+out["fixed_call_ms"] = fixed * 1e3
+for k, v in list(out.items()):
+    if isinstance(v, dict):
+        b = nb * (2 if k == "compare" else 1)
+        v["kernel_frac_of_8TBs_est"] = b / max(v["ms"] * 1e-3 - fixed, 1e-9) / 8e12
 print(json.dumps(out))
