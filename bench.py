@@ -274,10 +274,12 @@ def small_call_latency(n=1024, reps=300):
     lat = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["latency"]
     out = {"note": f"shmem_int_sum_to_all nreduce={n}, 2 PEs = 2 processes sharing this GPU, "
                    f"device-resident symmetric heaps, median of {reps} calls barrier to barrier"}
-    for k in ("fused_team", "team"):
+    for k in ("fused_team", "team", "host_fused_staged", "host_staged"):
         v = lat[f"{n}/{k}"]
         out[k + "_us"] = v["us_median"]
         out[k + "_correct"] = v["correct"]
+    out["note"] += ("; host_* = the same call on a pinned host symmetric heap (config 1's "
+                    "own placement): fused staged (one launch) vs pipelined STAGED")
     src = O.team_inputs("int", 2, n, 5, "bits")
     out["cpu_reference_loop_us"] = O.cpu_baseline("int", "sum", src, reps=2000, pin=True) * 1e6
     return out
