@@ -114,7 +114,7 @@ def _timer_sig(pet):
                                     ctypes.c_int]
 
 
-def host_staged_time(n, reps=5):
+def host_staged_time(n, reps=5, pes=2):
     """The reference's data placement: sources and targets in HOST symmetric
     heaps.  shmem_double_sum_to_all over a 2-PE set on one GPU (pthreads as
     PEs), STAGED path: H2D own source -> team exchange on the GPU -> D2H,
@@ -126,26 +126,28 @@ def host_staged_time(n, reps=5):
     from support import team as T
     L = osgpu.load()
     L.osgpu_finalize()
-    out = {"note": f"2 PEs (pthreads) on one GPU, host heaps, nreduce={n} doubles per PE; "
-                   f"PCIe bytes per call = 2*{n}*8 H2D + 2*{n}*8 D2H"}
+    P = pes
+    out = {"note": f"{P} PEs (pthreads) on one GPU, host heaps, nreduce={n} doubles per PE; "
+                   f"PCIe bytes per call = {P}*{n}*8 H2D + {P}*{n}*8 D2H"}
     for pinned in (True, False):
-        tm = T.Team(2, 2 * n * 8 + 8192, device=False)
+        tm = T.Team(P, 2 * n * 8 + 8192, device=False)
         toff = (n * 8 + 4095) // 4096 * 4096
-        for pe in range(2):
+        for pe in range(P):
             lo = tm.hoff + pe * tm.H
             tm.hbuf[lo:lo + n * 8].view(np.float64)[:] = 1.5 + pe
         if pinned:
-            assert L.osgpu_host_register(ctypes.c_void_p(tm.base), 2 * tm.H) == 0
+            assert L.osgpu_host_register(ctypes.c_void_p(tm.base), P * tm.H) == 0
         fn = ctypes.cast(L.shmem_double_sum_to_all, ctypes.c_void_p)
-        tgt = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
-        src = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
-        ps = (ctypes.c_void_p * 2)(tm.ptr(0, tm.psync_off), tm.ptr(1, tm.psync_off))
+        tgt = (ctypes.c_void_p * P)(*[tm.ptr(pe, toff) for pe in range(P)])
+        src = (ctypes.c_void_p * P)(*[tm.ptr(pe, 0) for pe in range(P)])
+        ps = (ctypes.c_void_p * P)(*[tm.ptr(pe, tm.psync_off) for pe in range(P)])
         _timer_sig(tm.pet)
-        sec = tm.pet.pet_time_to_all(fn, 2, tgt, src, ps, n, reps)
-        ok = bool((tm.hbuf[tm.hoff + toff: tm.hoff + toff + n * 8].view(np.float64) == 4.0).all())
+        sec = tm.pet.pet_time_to_all(fn, P, tgt, src, ps, n, reps)
+        want = sum(1.5 + pe for pe in range(P))
+        ok = bool((tm.hbuf[tm.hoff + toff: tm.hoff + toff + n * 8].view(np.float64) == want).all())
         out["pinned" if pinned else "pageable"] = {
             "ms_per_call": sec * 1e3,
-            "pcie_GBs_each_way": 2 * n * 8 / sec / 1e9,
+            "pcie_GBs_each_way": P * n * 8 / sec / 1e9,
             "algbw_GiBs_per_PE": n * 8 / sec / GIB,
             "correct": ok}
         if pinned:

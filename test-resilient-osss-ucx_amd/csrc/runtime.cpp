@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -398,6 +399,49 @@ void barrier(const Coll &c)
     DBG("%s PE %d: barrier enter", c.name, c.me);
     c.ops.barrier(c.PE_start, c.logPE_stride, c.PE_size, c.pSync);
     DBG("%s PE %d: barrier exit", c.name, c.me);
+}
+
+// Pageable host arrays: the runtime's own bounce copies move ~27 GB/s each
+// way; this path stages them through the PE's pinned bounce slots with a
+// multi-threaded memcpy instead (OSGPU_COPY_THREADS, default 4), so the DMA
+// always runs from pinned memory.
+bool host_pinned(const void *p)
+{
+    // OSGPU_HOST_BOUNCE=0: leave pageable memory to the runtime's own copies
+    static const int no_bounce = env_choice("OSGPU_HOST_BOUNCE", "0", 0);
+    if (no_bounce) return true;
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void) hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+void par_memcpy(void *dst, const void *src, size_t n)
+{
+    static const int nt = [] {
+        const char *e = getenv("OSGPU_COPY_THREADS");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : (v > 32 ? 32 : v);
+    }();
+    const size_t min_piece = (size_t) 1 << 20;
+    int k = (int) std::min<size_t>((size_t) nt, (n + min_piece - 1) / min_piece);
+    if (k <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t piece = (n / k + 4095) & ~(size_t) 4095;
+    std::vector<std::thread> th;
+    for (int i = 1; i < k; i++) {
+        const size_t lo = (size_t) i * piece;
+        if (lo >= n) break;
+        const size_t len = std::min(piece, n - lo);
+        th.emplace_back([=] { memcpy((char *) dst + lo, (const char *) src + lo, len); });
+    }
+    memcpy(dst, src, std::min(piece, n));
+    for (auto &t : th) t.join();
 }
 
 // ---------------------------------------------------------------------

@@ -124,6 +124,11 @@ void barrier(const Coll &c);
 
 // ---------------------------------------------------------- host staging
 
+// pinned (registered or hipHostMalloc) host memory?
+bool host_pinned(const void *p);
+// memcpy split over OSGPU_COPY_THREADS threads (default 4) for large copies
+void par_memcpy(void *dst, const void *src, size_t n);
+
 // Device staging of one PE for one active set: four slots of `slot` bytes,
 // mapped into every member PE (same process: raw pointer; other processes:
 // HIP IPC), exchanged once through spare pSync words (runtime.cpp).

@@ -9,8 +9,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 64 << 20
+PES = int(os.environ.get("SWEEP_PES", "2"))
 
-SETTINGS = [
+SETTINGS = [{}, {"OSGPU_HOST_BOUNCE": "0"}] if os.environ.get("SWEEP_BOUNCE") else [
     {},
     {"OSGPU_STAGE_BYTES": str(8 << 20)},
     {"OSGPU_STAGE_BYTES": str(128 << 20)},
@@ -19,7 +20,7 @@ SETTINGS = [
 ]
 
 CODE = ("import sys, json; sys.path.insert(0, %r); import bench; "
-        "print('RESULT ' + json.dumps(bench.host_staged_time(%d)))") % (ROOT, N)
+        "print('RESULT ' + json.dumps(bench.host_staged_time(%d, pes=%d)))") % (ROOT, N, PES)
 
 for s in SETTINGS:
     env = dict(os.environ, **s)
@@ -28,4 +29,4 @@ for s in SETTINGS:
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
     out = json.loads(line[0][7:]) if line else {"error": r.stderr[-500:]}
     out.pop("note", None)
-    print(json.dumps({"env": s, **out}), flush=True)
+    print(json.dumps({"env": s, "pes": PES, **out}), flush=True)
