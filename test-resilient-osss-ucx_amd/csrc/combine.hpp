@@ -12,7 +12,7 @@
 #define OSGPU_U_K4 4
 #endif
 #ifndef OSGPU_U_K8
-#define OSGPU_U_K8 2
+#define OSGPU_U_K8 4
 #endif
 
 namespace osgpu {

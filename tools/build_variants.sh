@@ -1,19 +1,23 @@
 #!/bin/bash
 # Build libosgpu_reduce variants with different per-lane unroll depths
 # (OSGPU_U_K2/K4/K8) into tools/variants/ for tools/variant_sweep.py.
+#   VARIANTS="421 442 444" tools/build_variants.sh   (digits: U for K<=2, K<=4, K<=8)
 set -e
 cd "$(dirname "$0")/../test-resilient-osss-ucx_amd/csrc"
 make -s -j8
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math"
-for v in "4 2 1" "4 4 2" "4 2 2" "4 4 1" "8 4 2"; do
-  set -- $v
-  tag="u$1$2$3"; d=../../tools/variants/$tag; mkdir -p $d
-  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$1 -DOSGPU_U_K4=$2 -DOSGPU_U_K8=$3 -c combine.hip -o $d/combine.o &
-  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$1 -DOSGPU_U_K4=$2 -DOSGPU_U_K8=$3 -c team.hip -o $d/team.o &
+TAGS=${VARIANTS:-"421 442 422 441 842"}
+for t in $TAGS; do
+  a=${t:0:1}; b=${t:1:1}; c=${t:2:1}
+  d=../../tools/variants/u$t; mkdir -p $d
+  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$a -DOSGPU_U_K4=$b -DOSGPU_U_K8=$c -c combine.hip -o $d/combine.o &
+  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$a -DOSGPU_U_K4=$b -DOSGPU_U_K8=$c -c team.hip -o $d/team.o &
 done
 wait
-for v in "4 2 1" "4 4 2" "4 2 2" "4 4 1" "8 4 2"; do
-  set -- $v; tag="u$1$2$3"; d=../../tools/variants/$tag
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so $d/combine.o $d/team.o longdouble.o shmem_reduce.o -lrccl -ldl -lpthread
+OTHERS="fused.o verify.o longdouble.o copy.o runtime.o shmem_reduce.o shmem_collect.o"
+for t in $TAGS; do
+  d=../../tools/variants/u$t
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
+      $d/combine.o $d/team.o $OTHERS -lrccl -ldl -lpthread
 done
 ls ../../tools/variants/*/libosgpu_reduce.so
