@@ -154,12 +154,14 @@ class Team:
         then check every member's pSync is back at SHMEM_SYNC_VALUE."""
         errs = []
         self.last_paths = {}
+        self.last_coll_paths = {}
 
         def body(pe):
             try:
                 self.pet.pet_set_me(pe)
                 call(pe)
                 self.last_paths[pe] = self.osgpu.last_path()
+                self.last_coll_paths[pe] = self.osgpu.last_coll_path()
             except Exception as e:  # pragma: no cover
                 errs.append(e)
 
