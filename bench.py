@@ -825,6 +825,29 @@ def bench_multi(args):
                           "GiBs_per_PE_incl_H2D_D2H": 3 * n5 * 4 / tt / GIB,
                           "parity": _sample_parity(rank, world, h5s, h5t, n5, op, dist,
                                                    t="float")}
+            # the copy-free figure: the same calls on
+            # the device heaps, exact team kernel over xGMI
+            if team_ok and n5 * 4 <= seg_bytes:
+                L.osgpu_set_path(osgpu.PATH_P2P)
+                d5s = hsrc[: n5 * 4].view(torch.float32)
+                d5t = htgt[: n5 * 4].view(torch.float32)
+                gd = torch.Generator(device=dev).manual_seed(97 + rank)
+                cf = {"placement": "device heaps (HBM), p2p-team"}
+                for op, lo, hi in (("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1)):
+                    d5s.uniform_(lo, hi, generator=gd)
+                    torch.cuda.synchronize()
+                    f5 = getattr(L, f"shmem_float_{op}_to_all")
+
+                    def step5d():
+                        f5(d5t.data_ptr(), d5s.data_ptr(), n5, 0, 0, world, wrk, psync)
+
+                    tt = _timed(step5d, 3, 1, dist, torch)
+                    cf[op] = {"ms_per_call": tt / 3 * 1e3,
+                              "GiBs_per_PE": 3 * n5 * 4 / tt / GIB,
+                              "parity": _sample_parity(rank, world, d5s, d5t, n5, op, dist,
+                                                       t="float")}
+                c5["copy_free"] = cf
+                L.osgpu_set_path(osgpu.PATH_AUTO)
             res["config5"] = c5
             _log(rank, "config5 done")
         except Exception as e:
