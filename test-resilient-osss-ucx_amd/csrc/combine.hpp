@@ -60,6 +60,8 @@ constexpr int kFlagDone = 8;      // [8, 16): done[member]
 constexpr int kFlagTicket = 16;   // last-workgroup tickets (u32): completion,
 constexpr int kFlagTicketIn = 17;  //   staged copy-in,
 constexpr int kFlagTicketOut = 18; //   staged copy-out
+constexpr int kFlagCount = 20;    // [20, 28): count[member] (collect: tag << 40 | source bytes)
+constexpr int kCountBits = 40;
 constexpr int kFlagWords = 32;
 // fused grids: at most one workgroup of 256 lanes per CU of the GPU (256 on
 // MI355X), split between the members sharing it (one member per GPU: all)
@@ -87,9 +89,19 @@ struct FusedArgs {
     // copy form (launch_fused_copy): nseg segments src[d] -> dst[d]
     size_t seg_bytes[kMaxTeam];
     int nseg;
+    // collect form (launch_fused_collect): src[i] every member's source,
+    // dst[0] my output; contributions differ per member and are exchanged
+    // in the flag areas at arrival
+    size_t my_count;                      // bytes of my source (< 2^kCountBits)
+    unsigned long long count_tag;         // the set's collect sequence number
+    size_t src_avail[kMaxTeam];           // bytes mapped from src[i] (bounds)
+    size_t copy_limit;                    // copy in the launch iff the total fits
+    unsigned long long *counts_host;      // host-mapped: every member's count, then
+                                          //   counts_host[kMaxTeam] = 1 if copied
 };
 bool fused_supported(int type);
 hipError_t launch_fused_copy(const FusedArgs &a, hipStream_t s);
+hipError_t launch_fused_collect(const FusedArgs &a, hipStream_t s);
 hipError_t launch_fused(int type, int op, const FusedArgs &a, hipStream_t s);
 
 // Full-size parity checks on the GPU (verify.hip).  Checksum of n elements

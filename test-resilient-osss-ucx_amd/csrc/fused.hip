@@ -11,7 +11,8 @@
 // IPC-mapped into every member, runtime.cpp sync_setup):
 //   words [0, 8)   arrive[i]: epoch of the last call member i entered
 //   words [8, 16)  done[i]:   epoch of the last call member i finished
-//   word  16       ticket:    last-workgroup election inside one launch
+//   words 16-18    tickets:   last-workgroup elections inside one launch
+//   words [20, 28) count[i]:  collect only, member i's contribution + tag
 // Epochs grow by one per fused call on the set, so nothing is ever reset
 // (pSync stays at SHMEM_SYNC_VALUE, untouched).
 //
@@ -245,6 +246,101 @@ __global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
     fused_done(a, s_go);
 }
 
+// Grid-stride copy of one piece at the widest width both ends allow.
+__device__ __forceinline__ void copy_piece(char *dst, const char *src, size_t nb, size_t tid,
+                                           size_t stride)
+{
+    const uintptr_t al = (uintptr_t) src | (uintptr_t) dst;
+    size_t done = 0;
+    if ((al & 15) == 0) {
+        const size_t nv = nb / 16;
+        for (size_t j = tid; j < nv; j += stride)
+            store_out(reinterpret_cast<u32x4 *>(dst) + j,
+                      __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src) + j));
+        done = nv * 16;
+    } else if ((al & 7) == 0) {
+        const size_t nw = nb / 8;
+        for (size_t j = tid; j < nw; j += stride)
+            reinterpret_cast<unsigned long long *>(dst)[j] =
+                reinterpret_cast<const unsigned long long *>(src)[j];
+        done = nw * 8;
+    } else if ((al & 3) == 0) {
+        const size_t nw = nb / 4;
+        for (size_t j = tid; j < nw; j += stride)
+            reinterpret_cast<unsigned *>(dst)[j] = reinterpret_cast<const unsigned *>(src)[j];
+        done = nw * 4;
+    }
+    for (size_t b = done + tid; b < nb; b += stride) dst[b] = src[b];
+}
+
+// collect (shmem_collect.cpp, src/shmemc/collect.c:24-69): contributions
+// differ per member, so the counts ARE the arrival: workgroup 0 writes
+// (tag << 40 | count) into slot me of every member's area, tag = the set's
+// collect sequence number (the same on every member; consecutive collects
+// differ by one, so a slot holds this call's count or the previous one's --
+// no member writes the next before every member has passed this call's done
+// barrier, which follows its reads).  Lanes i < P of every workgroup wait
+// for slot i to carry this call's tag.  All members see the same counts, so
+// they all make the same choice: if the gathered total fits copy_limit the
+// pieces are copied here (member i's source to my output at the prefix
+// offset of i); otherwise the launch is only the count exchange and the
+// entry barrier, and the host copies.  The host learns the counts (and the
+// choice) from counts_host.  arrive[] is not written: epochs only grow, so
+// the next fused call's wait (arrive >= E') is unaffected.
+__global__ __launch_bounds__(kFBlock) void fused_collect_kernel(FusedArgs a)
+{
+    __shared__ int s_go;
+    __shared__ unsigned long long s_cnt[kMaxTeam];
+    constexpr unsigned long long kCountMask = (1ull << kCountBits) - 1;
+    const unsigned long long tag = a.count_tag & ((1ull << (64 - kCountBits)) - 1);
+    if (threadIdx.x == 0) s_go = 1;
+    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
+        st_sys(a.flags[threadIdx.x] + kFlagCount + a.me,
+               tag << kCountBits | ((unsigned long long) a.my_count & kCountMask));
+    __syncthreads();
+    if ((int) threadIdx.x < a.P) {
+        const unsigned long long *w = a.mine + kFlagCount + threadIdx.x;
+        const unsigned long long t0 = (unsigned long long) wall_clock64();
+        unsigned long long v;
+        while (((v = ld_sys(w)) >> kCountBits) != tag) {
+            if ((unsigned long long) wall_clock64() - t0 > a.timeout) {
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_go = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_cnt[threadIdx.x] = v & kCountMask;
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    __syncthreads();
+    if (!s_go) return;
+    unsigned long long total = 0;
+    bool fits = true;
+    for (int i = 0; i < a.P; i++) {
+        total += s_cnt[i];
+        fits = fits && s_cnt[i] <= a.src_avail[i];
+    }
+    const bool copy = fits && total <= a.copy_limit;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int i = 0; i < a.P; i++) st_sys(a.counts_host + i, s_cnt[i]);
+        st_sys(a.counts_host + kMaxTeam, copy ? 1ull : 0ull);
+        if (!fits) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (copy) {
+        const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
+        const size_t stride = (size_t) gridDim.x * kFBlock;
+        char *out = static_cast<char *>(a.dst[0]);
+        size_t off = 0;
+        for (int i = 0; i < a.P; i++) {
+            if (s_cnt[i]) copy_piece(out + off, static_cast<const char *>(a.src[i]), s_cnt[i],
+                                     tid, stride);
+            off += s_cnt[i];
+        }
+    }
+    fused_done(a, s_go);
+}
+
 template <typename T, int OP, bool VEC>
 __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
 {
@@ -426,6 +522,21 @@ hipError_t launch_fused_copy(const FusedArgs &a0, hipStream_t s)
     if (blocks < 1) blocks = 1;
     if (blocks > (size_t) a.max_blocks) blocks = (size_t) a.max_blocks;
     hipLaunchKernelGGL(fused_copy_kernel, dim3((unsigned) blocks), dim3(kFBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_collect(const FusedArgs &a, hipStream_t s)
+{
+    if (a.P < 2 || a.P > kMaxTeam || a.me < 0 || a.me >= a.P || a.max_blocks < 1 ||
+        a.max_blocks > kFusedBlocksPerGpu || !a.counts_host || !a.dst[0])
+        return hipErrorInvalidValue;
+    // pieces are copied one after another, each grid-stride: sized by my
+    // estimate of one piece (contributions like mine), as the fused copy
+    const size_t est = a.my_count < a.copy_limit ? a.my_count : a.copy_limit;
+    size_t blocks = (est / 16 + kFBlock - 1) / kFBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (size_t) a.max_blocks) blocks = (size_t) a.max_blocks;
+    hipLaunchKernelGGL(fused_collect_kernel, dim3((unsigned) blocks), dim3(kFBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -696,7 +696,10 @@ bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool w
     const bool incomplete = word && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < epoch;
     if (!err && !incomplete) return true;
     char msg[256];
-    if (err)
+    if (err == 3)
+        snprintf(msg, sizeof(msg),
+                 "collect: a member's contribution exceeds its source object in the heap");
+    else if (err)
         snprintf(msg, sizeof(msg),
                  "device barrier (%s) timed out: a member of the active set did not enter or "
                  "finish the call", err == 1 ? "entry" : "exit");
@@ -732,14 +735,16 @@ SyncSet *sync_setup(const Coll &c)
     bool ok = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess;
     if (!ok) (void) hipGetLastError();
     if (ok && hipMemset(p, 0, bytes) != hipSuccess) ok = false;
-    if (ok && hipHostMalloc((void **) &S.err_h, sizeof(int) * 16,
+    if (ok && hipHostMalloc((void **) &S.err_h, sizeof(int) * 64,
                             hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         ok = false;
-    if (ok) {  // word 0: error code; words 8..9: completion epoch
-        memset(S.err_h, 0, sizeof(int) * 16);
+    if (ok) {  // int 0: error code; ints 8..9: completion epoch; 16..33: collect counts
+        memset(S.err_h, 0, sizeof(int) * 64);
         S.done_h = reinterpret_cast<unsigned long long *>(S.err_h + 8);
+        S.cnt_h = reinterpret_cast<unsigned long long *>(S.err_h + 16);
         ok = hipHostGetDevicePointer((void **) &S.err_d, S.err_h, 0) == hipSuccess;
         S.done_d = reinterpret_cast<unsigned long long *>(S.err_d + 8);
+        S.cnt_d = reinterpret_cast<unsigned long long *>(S.err_d + 16);
     }
     int rate_khz = 0;
     if (ok) ok = hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) ==

@@ -167,10 +167,12 @@ struct SyncSet {
     std::vector<unsigned long long *> peer;    // by active-set index
     std::vector<void *> opened;                // IPC mappings to close
     unsigned long long epoch = 0;
+    unsigned long long ncollect = 0;           // collect calls on the set (count tags)
     int rate_khz = 0;                          // wall clock of the device
     int max_blocks = 0;                        // workgroups per fused launch
     int *err_h = nullptr, *err_d = nullptr;    // host-mapped error word
     unsigned long long *done_h = nullptr, *done_d = nullptr;  // host-mapped completion epoch
+    unsigned long long *cnt_h = nullptr, *cnt_d = nullptr;    // host-mapped collect counts
 };
 SyncSet *sync_setup(const Coll &c);
 // wait for a fused launch's completion word (epoch) / report a failed one

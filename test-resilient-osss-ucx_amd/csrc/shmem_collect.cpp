@@ -33,8 +33,11 @@
 //           algorithm over the runtime's shmem_getmem -- pure byte movement,
 //           which the runtime's memcpy does at memory speed.
 //
-// collect needs every PE's nelems before any byte moves: each PE publishes
-// it in a spare pSync word (the reference's barrier uses pSync[0] only,
+// collect needs every PE's nelems before any byte moves.  On device heaps
+// the counts ride on the device-side arrival of a fused launch (fused.hip
+// fused_collect_kernel), which also moves the pieces when the gathered total
+// is within the fused limit.  Otherwise each PE publishes its count in a
+// spare pSync word (the reference's barrier uses pSync[0] only,
 // src/shmemc/barrier.c:64-97), reads its peers' with shmem_getmem after the
 // first barrier and clears its word after the last -- pSync is returned at
 // SHMEM_SYNC_VALUE, as the reference's wavefront leaves it (collect.c:67).
@@ -231,6 +234,79 @@ void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg
     if (!fused_check(c.name, S, a.epoch, !scratch)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
 }
 
+// collect on device heaps as ONE launch (fused.hip fused_collect_kernel):
+// the counts ride on the device arrival instead of pSync + getmem + a host
+// barrier.  Every member reaches the same outcome (the choice depends on
+// the exchanged counts and the shared fused limit only):
+//   2  the whole call ran in the launch (or failed, reported);
+//   1  the launch exchanged the counts (c.src_len) and passed the entry
+//      barrier; the pieces are left to the COPY path (total over the limit);
+//   0  not eligible: the host exchanges the counts.
+int fused_collect(CCall &c)
+{
+    const int em = entry_mode();
+    const size_t lim = fused_max_bytes();
+    const int P = c.PE_size;
+    if (!(em == ENTRY_STREAM || em == ENTRY_NONE) || P < 2 || P > osgpu::kMaxTeam ||
+        !c.ops.getmem || lim == 0)
+        return 0;
+    // every member's source object; its length is not known yet, so the
+    // bytes from it to the end of its heap segment bound what may be read
+    const size_t mine = c.nelems * c.esz;
+    int seg = -1;
+    size_t off = 0;
+    if (!heap_locate(c.me, c.source, mine ? mine : 1, &seg, &off)) return 0;
+    osgpu::FusedArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int i = 0; i < P; i++) {
+        HeapEntry h;
+        if (!heap_segment(c.pe_at(i), seg, &h) || off >= h.bytes) return 0;
+        a.src[i] = h.base + off;
+        a.src_avail[i] = h.bytes - off;
+    }
+    SyncSet *S = sync_setup(c);
+    if (!S) return 0;
+    hipStream_t st = pe_stream(c.name, c.me);
+    // my output: the target, or scratch when the target (at most `lim` bytes
+    // if copied here) may overlap my source, which peers read in the launch
+    const bool scratch = overlap2(c.target, lim, c.source, mine);
+    char *out = scratch ? (char *) device_scratch(c.name, c.me, lim) : (char *) c.target;
+    for (int i = 0; i < P; i++) a.flags[i] = S->peer[i];
+    a.dst[0] = out;
+    a.mine = S->local;
+    a.err = S->err_d;
+    a.done_host = S->done_d;
+    a.counts_host = S->cnt_d;
+    a.epoch = ++S->epoch;
+    a.timeout = fused_timeout_ticks(*S);
+    a.P = P;
+    a.me = S->idx;
+    a.max_blocks = S->max_blocks;
+    if (mine >> osgpu::kCountBits) fatal(c.name, "contribution of %zu bytes too large", mine);
+    a.my_count = mine;
+    a.count_tag = ++S->ncollect;
+    a.copy_limit = lim;
+    DBG("%s PE %d: fused collect, %zu bytes mine, epoch %llu", c.name, c.me, mine, a.epoch);
+    entry_order(c.name, st);
+    hipError_t e = osgpu::launch_fused_collect(a, st);
+    if (e != hipSuccess) fatal(c.name, "fused collect launch: %s", hipGetErrorString(e));
+    fused_wait(c.name, *S, st, a.epoch);
+    if (!fused_check(c.name, *S, a.epoch, true)) {
+        t_last_coll = OSGPU_RAN_FUSED_FAILED;
+        return 2;
+    }
+    c.src_len.assign(P, 0);
+    size_t total = 0;
+    for (int i = 0; i < P; i++) total += (c.src_len[i] = (size_t) S->cnt_h[i]);
+    if (!S->cnt_h[osgpu::kMaxTeam]) return 1;
+    t_last_coll = OSGPU_RAN_FUSED_COPY;
+    if (scratch && total) {  // every reader of my source is done: the launch passed done
+        HIPCHK(c.name, hipMemcpyAsync(c.target, out, total, hipMemcpyDeviceToDevice, st));
+        stream_wait(c.name, st);
+    }
+    return 2;
+}
+
 void run_copy(const CCall &c, const std::vector<const char *> &src, bool counts_done)
 {
     hipStream_t st = pe_stream(c.name, c.me);
@@ -411,11 +487,20 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
     const MemKind kt = mem_kind(target, &dt), ks = mem_kind(source, &ds);
     if (kt != ks) fatal(name, "target and source must both be device or both be host memory");
 
-    bool counts_done = false;
-    if (kind == K_COLLECT) {
+    bool counts_done = false, psync_counts = false;
+    if (kind == K_COLLECT && kt == MEM_DEVICE) {  // counts on the device arrival
+        int cur = 0;
+        HIPCHK(name, hipGetDevice(&cur));
+        if (cur != dt) HIPCHK(name, hipSetDevice(dt));
+        const int f = fused_collect(c);
+        if (cur != dt) HIPCHK(name, hipSetDevice(cur));
+        if (f == 2) return;
+        counts_done = f == 1;
+    }
+    if (kind == K_COLLECT && !counts_done) {
         if (kt == MEM_DEVICE) entry_sync(name);  // my source is final before I publish
         exchange_counts(c);                      // includes the first barrier
-        counts_done = true;
+        counts_done = psync_counts = true;
     }
     plan(c);
     size_t moved = 0;
@@ -423,7 +508,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
     if (moved == 0) {  // a collect of empty contributions only synchronises
         t_last_coll = OSGPU_RAN_BARRIER_ONLY;
         barrier(c);
-        c.pSync[kCountWord] = 0;
+        if (psync_counts) c.pSync[kCountWord] = 0;
         return;
     }
 
@@ -445,7 +530,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
         if (S && (force_staged || S->ndev == c.PE_size || c.PE_size == 1)) run_staged(c, *S);
         else run_getmem(c);
         barrier(c);
-        if (kind == K_COLLECT) c.pSync[kCountWord] = 0;
+        if (psync_counts) c.pSync[kCountWord] = 0;
         return;
     }
 
@@ -467,7 +552,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
                   ? " or an RCCL communicator over the whole job"
                   : "");
     }
-    if (kind == K_COLLECT) c.pSync[kCountWord] = 0;
+    if (psync_counts) c.pSync[kCountWord] = 0;
     if (cur != dt) HIPCHK(name, hipSetDevice(cur));
 }
 

@@ -219,7 +219,13 @@ def device_heap_modes(L, PES, mode, rank, world):
         from support import coll_cases as CC
         import oracle_coll as OC
         digests, paths = {}, {}
-        for ci, c in enumerate(CC.fused_cases()):
+        # second pass: collect again under a 256-B fused limit -- the launch
+        # then only exchanges the counts when the gathered total is larger
+        runs = [(str(ci), c, -1) for ci, c in enumerate(CC.fused_cases())]
+        runs += [(f"{ci}/big", c, 256) for ci, c in enumerate(CC.fused_cases())
+                 if c["kind"] == "collect"]
+        for ci, c, lim in runs:
+            L.osgpu_set_fused_max_bytes(lim)
             npes, start, log, size = c["set"]
             if npes > world:
                 continue
@@ -239,12 +245,13 @@ def device_heap_modes(L, PES, mode, rank, world):
                     f(dev0 + tgt_off, dev0 + src_off, cnt, c["root"], start, log, size, psync)
                 else:
                     f(dev0 + tgt_off, dev0 + src_off, cnt, start, log, size, psync)
-                paths[str(ci)] = osgpu.last_coll_path()
+                paths[ci] = osgpu.last_coll_path()
                 assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
             if rank < npes:
                 got = heap[tgt_off - CC.MARGIN:tgt_off + tgt_bytes + CC.MARGIN].cpu().numpy()
-                digests[str(ci)] = hashlib.sha256(got.tobytes()).hexdigest()
+                digests[ci] = hashlib.sha256(got.tobytes()).hexdigest()
             sync()
+        L.osgpu_set_fused_max_bytes(-1)
         res["digests"], res["paths"] = digests, paths
     if mode == "golden":
         # around a 64 KiB fused limit: under, at, just over
@@ -348,7 +355,7 @@ def device_heap_modes(L, PES, mode, rank, world):
                                       "path": ran, "correct": ok}
             # data-movement collectives on the same device heaps: fused copy
             # (one launch) vs the copy kernel between host barriers
-            for kind in ("fcollect", "broadcast", "alltoall"):
+            for kind in ("fcollect", "collect", "broadcast", "alltoall"):
                 f = osgpu.coll(kind, 32)
                 ne = n // world if kind == "alltoall" else n
                 coff = (world * n * 4 + 4095) // 4096 * 4096 + (8 << 20)

@@ -248,11 +248,13 @@ def test_fused_staged_golden_processes(tmp_path):
 
 @pytest.mark.gpu
 def test_fused_collectives_processes(tmp_path):
-    """broadcast / fcollect / alltoall (32/64) with one process per PE (8 on
-    cuda:0, IPC device heaps): small calls run as one launch with the
-    device-side barriers (fused copy); collect keeps its count exchange and
-    host barriers.  Every member's target region, margins included, must
-    equal the restatement's (oracle/oracle_coll.py)."""
+    """broadcast / collect / fcollect / alltoall (32/64) with one process per
+    PE (8 on cuda:0, IPC device heaps): small calls run as one launch with
+    the device-side barriers (fused copy; collect's counts ride on the device
+    arrival).  collect again under a 256-B limit: the launch exchanges the
+    counts and the COPY path moves the larger totals.  Every member's target
+    region, margins included, must equal the restatement's
+    (oracle/oracle_coll.py)."""
     import hashlib
     import torch
     if not torch.cuda.is_available():
@@ -260,19 +262,27 @@ def test_fused_collectives_processes(tmp_path):
     from support import coll_cases as CC
     world = 8
     res = launch("collgolden", world, tmp_path)
-    nfused = 0
+    nfused = nbig = 0
     for ci, c in enumerate(CC.fused_cases()):
         if c["set"][0] > world:
             continue
         exp = CC.fused_expected(c)
-        for r in range(c["set"][0]):
-            want = hashlib.sha256(exp[r].tobytes()).hexdigest()
-            assert res[r]["digests"][str(ci)] == want, (c, r)
-            ran = res[r]["paths"].get(str(ci))
-            if ran is not None:
-                assert ran == ("copy" if c["kind"] == "collect" else "fused_copy"), (c, r, ran)
-                nfused += ran == "fused_copy"
-    assert nfused > 600, nfused
+        keys = [str(ci)] + ([f"{ci}/big"] if c["kind"] == "collect" else [])
+        total = sum(CC.fused_counts(c).values()) * c["bits"] // 8
+        for key in keys:
+            for r in range(c["set"][0]):
+                want = hashlib.sha256(exp[r].tobytes()).hexdigest()
+                assert res[r]["digests"][key] == want, (c, key, r)
+                ran = res[r]["paths"].get(key)
+                if ran is None:
+                    continue
+                if key.endswith("/big") and total > 256:
+                    assert ran == "copy", (c, key, r, ran)
+                    nbig += 1
+                else:
+                    assert ran == "fused_copy", (c, key, r, ran)
+                    nfused += 1
+    assert nfused > 800 and nbig > 100, (nfused, nbig)
 
 
 @pytest.mark.gpu
