@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -419,6 +420,11 @@ bool host_pinned(const void *p)
     return a.type == hipMemoryTypeHost;
 }
 
+// Helper threads are capped process-wide (OSGPU_COPY_THREADS_TOTAL, default
+// 8): with many PE threads copying at once, more threads than that only
+// contend for the same memory channels.
+std::atomic<int> g_copy_helpers{0};
+
 void par_memcpy(void *dst, const void *src, size_t n)
 {
     static const int nt = [] {
@@ -426,12 +432,27 @@ void par_memcpy(void *dst, const void *src, size_t n)
         const int v = e ? atoi(e) : 4;
         return v < 1 ? 1 : (v > 32 ? 32 : v);
     }();
+    static const int cap = [] {
+        const char *e = getenv("OSGPU_COPY_THREADS_TOTAL");
+        const int v = e ? atoi(e) : 8;
+        return v < 0 ? 0 : (v > 256 ? 256 : v);
+    }();
     const size_t min_piece = (size_t) 1 << 20;
-    int k = (int) std::min<size_t>((size_t) nt, (n + min_piece - 1) / min_piece);
-    if (k <= 1) {
+    const int want = (int) std::min<size_t>((size_t) nt, (n + min_piece - 1) / min_piece) - 1;
+    int got = 0;  // helpers reserved under the cap
+    for (int cur = g_copy_helpers.load(); want > 0;) {
+        got = std::min(want, cap - cur);
+        if (got <= 0) {
+            got = 0;
+            break;
+        }
+        if (g_copy_helpers.compare_exchange_weak(cur, cur + got)) break;
+    }
+    if (got == 0) {
         memcpy(dst, src, n);
         return;
     }
+    const int k = got + 1;
     const size_t piece = (n / k + 4095) & ~(size_t) 4095;
     std::vector<std::thread> th;
     for (int i = 1; i < k; i++) {
@@ -442,6 +463,7 @@ void par_memcpy(void *dst, const void *src, size_t n)
     }
     memcpy(dst, src, std::min(piece, n));
     for (auto &t : th) t.join();
+    g_copy_helpers.fetch_sub(got);
 }
 
 // ---------------------------------------------------------------------

@@ -11,7 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 64 << 20
 PES = int(os.environ.get("SWEEP_PES", "2"))
 
-SETTINGS = [{}, {"OSGPU_HOST_BOUNCE": "0"}] if os.environ.get("SWEEP_BOUNCE") else [
+SETTINGS = json.loads(os.environ["SWEEP_SETTINGS"]) if os.environ.get("SWEEP_SETTINGS") else \
+    [{}, {"OSGPU_HOST_BOUNCE": "0"}] if os.environ.get("SWEEP_BOUNCE") else [
     {},
     {"OSGPU_STAGE_BYTES": str(8 << 20)},
     {"OSGPU_STAGE_BYTES": str(128 << 20)},
