@@ -82,7 +82,8 @@ def fused_cases():
     for kind in KINDS:
         for bits in (32, 64):
             for setdef in FUSED_SETS:
-                for nelems in (1, 63, 1001, 4099):
+                for nelems in ((0, 1, 63, 1001, 4099) if kind == "collect" else
+                               (1, 63, 1001, 4099)):
                     root = nelems % setdef[3] if kind == "broadcast" else 0
                     out.append({"kind": kind, "bits": bits, "set": setdef, "nelems": nelems,
                                 "root": root, "same": False, "seed": nelems + bits})
