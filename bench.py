@@ -749,6 +749,37 @@ def bench_multi(args):
     else:
         res["team_error"] = "HIP IPC export/import of the device heaps failed on some rank"
 
+    # ---- the local fold alone on every GPU at once (config 2's kernel: my
+    # source + a second resident array, K = 2, no exchange).  The north
+    # star's ">= 6x aggregate at 8 GPUs" is a property of this fold; `value`
+    # above is the whole to_all, whose exchange is xGMI-bound.
+    if not args.no_extra:
+        state["phase"] = "local_fold"
+        try:
+            other = htgt[: n * 8].view(torch.float64)
+            other.uniform_(1.0, 2.0, generator=torch.Generator(device=dev).manual_seed(3 + rank))
+            lout = torch.empty(n, dtype=torch.float64, device=dev)
+            srcs2 = (ctypes.c_void_p * 2)(src.data_ptr(), other.data_ptr())
+
+            def fold_step():
+                L.osgpu_combine(5, 0, lout.data_ptr(), srcs2, 2, n, None)
+
+            tl = _timed(fold_step, args.steps, args.warmup, dist, torch)
+            ok = bool(torch.equal(lout[:4096], src[:4096] + other[:4096]))
+            res["local_fold_all_gpus"] = {
+                "GiBs_aggregate": world * args.steps * 3 * n * 8 / tl / GIB,
+                "GBs_per_gpu": args.steps * 3 * n * 8 / tl / 1e9,
+                "frac_of_8TBs_per_gpu": args.steps * 3 * n * 8 / tl / 1e9 / HBM_PEAK_GBS,
+                "correct_sample_all_ranks": _agree(dist, world, ok),
+                "note": "combine_vec_kernel<double,SUM,2> on every GPU at once, 3*nreduce*8 B "
+                        "per GPU per step, max-over-ranks time; no exchange (compare with N=1 "
+                        "value for the fold's scaling)"}
+            del lout
+            torch.cuda.empty_cache()
+            _log(rank, "local fold done")
+        except Exception as e:
+            res["local_fold_all_gpus"] = {"error": repr(e)[:300]}
+
     # ---- RCCL on the same buffers, then BASELINE config 4 (1 Gi per PE)
     rccl_ok = False
     if not args.no_rccl:
