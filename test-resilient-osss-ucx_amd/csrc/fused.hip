@@ -223,10 +223,25 @@ __device__ __forceinline__ void fused_done(const FusedArgs &a, int &s_go)
 // The data-movement collectives' small calls (shmem_collect.cpp): the pieces
 // of my target pulled from every member's source, between the same device
 // barriers.  Segment d: a.seg_bytes[d] bytes from a.src[d] to a.dst[d].
+// Staged form (host heaps): my host source is first copied into my device
+// staging slot by the whole grid, the last workgroup arrives; the segments
+// then read the members' staging slots and write my host target directly.
 __global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
 {
     __shared__ int s_go;
-    if (!fused_arrive(a, s_go)) return;
+    if (a.host_in) {
+        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
+            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
+        if (threadIdx.x == 0)
+            s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
+        __syncthreads();
+        if (!s_go) return;
+    } else if (!fused_arrive(a, s_go)) {
+        return;
+    }
     const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
     const size_t stride = (size_t) gridDim.x * kFBlock;
     for (int d = 0; d < a.nseg; d++) {
@@ -516,7 +531,7 @@ hipError_t launch_fused_copy(const FusedArgs &a0, hipStream_t s)
     if (a.P < 2 || a.P > kMaxTeam || a.nseg < 0 || a.nseg > kMaxTeam || a.me < 0 ||
         a.me >= a.P || a.max_blocks < 1 || a.max_blocks > kFusedBlocksPerGpu)
         return hipErrorInvalidValue;
-    size_t most = 0;
+    size_t most = a.host_in ? a.host_bytes : 0;
     for (int d = 0; d < a.nseg; d++) most = a.seg_bytes[d] > most ? a.seg_bytes[d] : most;
     size_t blocks = (most / 16 + kFBlock - 1) / kFBlock;
     if (blocks < 1) blocks = 1;

@@ -185,6 +185,18 @@ bool device_sources(const CCall &c, std::vector<const char *> &src)
     return true;
 }
 
+// Bytes a call moves into targets, a figure every member computes alike:
+// broadcast nb, fcollect / alltoall P * nb, collect the gathered total.
+size_t shared_bytes(const CCall &c)
+{
+    const size_t nb = c.nelems * c.esz;
+    if (c.kind == K_BCAST) return nb;
+    if (c.kind != K_COLLECT) return (size_t) c.PE_size * nb;
+    size_t t = 0;
+    for (size_t l : c.src_len) t += l;
+    return t;
+}
+
 // Small broadcast / fcollect / alltoall calls run as ONE launch with the
 // reduce path's device-side barriers (fused.hip fused_copy_kernel).  The
 // decision uses only arguments every member shares (never which member I
@@ -192,10 +204,8 @@ bool device_sources(const CCall &c, std::vector<const char *> &src)
 bool fused_copy_eligible(const CCall &c)
 {
     const int em = entry_mode();
-    const size_t nb = c.nelems * c.esz;
-    const size_t bytes = c.kind == K_BCAST ? nb : (size_t) c.PE_size * nb;
     return (em == ENTRY_STREAM || em == ENTRY_NONE) && c.kind != K_COLLECT &&
-           c.PE_size >= 2 && c.PE_size <= osgpu::kMaxTeam && bytes <= fused_max_bytes() &&
+           c.PE_size >= 2 && c.PE_size <= osgpu::kMaxTeam && shared_bytes(c) <= fused_max_bytes() &&
            c.ops.getmem != nullptr;
 }
 
@@ -232,6 +242,58 @@ void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg
         fused_wait(c.name, S, st, a.epoch);
     }
     if (!fused_check(c.name, S, a.epoch, !scratch)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
+}
+
+// Host heaps pinned on every PE (osgpu_host_register): a small broadcast /
+// fcollect / alltoall as ONE launch -- my host source copied into my device
+// staging area, the device barriers, every piece pulled from the members'
+// staging areas straight into my host target (the STAGED path's H2D,
+// exchange and D2H, like the reduce's fused staged form).  My source is in
+// staging before I arrive and peers read only staging, so a target that
+// overlaps my source needs no temporary.  false: not taken (same verdict on
+// every member: shared sizes, and the heap pinned on every PE).
+bool run_fused_staged_copy(const CCall &c, StageSet &G)
+{
+    if (!fused_copy_eligible(c)) return false;
+    const size_t mine = c.src_len[c.idx];
+    size_t most = 0;  // the largest source, the same figure on every member
+    for (size_t l : c.src_len) most = std::max(most, l);
+    if (most > 4 * G.slot) return false;
+    void *hin = mine ? host_device_view(c.source, mine) : nullptr;
+    void *hout = c.out_bytes ? host_device_view(c.target, c.out_bytes) : nullptr;
+    if ((mine && !hin) || (c.out_bytes && !hout)) return false;
+    SyncSet *S = sync_setup(c);
+    if (!S) return false;
+    t_last_coll = OSGPU_RAN_FUSED_STAGED;
+    osgpu::FusedArgs a;
+    memset(&a, 0, sizeof(a));
+    for (const Piece &p : c.pieces) {
+        if (!p.len) continue;
+        a.src[a.nseg] = G.region(p.from) + p.src_off;
+        a.dst[a.nseg] = (char *) hout + p.dst_off;
+        a.seg_bytes[a.nseg] = p.len;
+        a.nseg++;
+    }
+    a.host_in = hin;
+    a.stage_mine = G.region(c.idx);
+    a.host_bytes = mine;
+    for (int i = 0; i < c.PE_size; i++) a.flags[i] = S->peer[i];
+    a.mine = S->local;
+    a.err = S->err_d;
+    a.done_host = S->done_d;
+    a.epoch = ++S->epoch;
+    a.timeout = fused_timeout_ticks(*S);
+    a.P = c.PE_size;
+    a.me = S->idx;
+    a.max_blocks = S->max_blocks;
+    DBG("%s PE %d: fused staged copy, %d pieces, epoch %llu", c.name, c.me, a.nseg, a.epoch);
+    hipStream_t st = pe_stream(c.name, c.me);
+    entry_order(c.name, st);
+    hipError_t e = osgpu::launch_fused_copy(a, st);
+    if (e != hipSuccess) fatal(c.name, "fused staged copy launch: %s", hipGetErrorString(e));
+    fused_wait(c.name, *S, st, a.epoch);
+    if (!fused_check(c.name, *S, a.epoch, true)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
+    return true;
 }
 
 // collect on device heaps as ONE launch (fused.hip fused_collect_kernel):
@@ -518,17 +580,26 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
             fatal(name, "no GPU visible: the collectives run on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
         // STAGED moves 1 + P (in + out) bytes per target byte over each
-        // PE's PCIe link; that beats the runtime's memcpy only when every
-        // member has a GPU (and a link) of its own -- PEs sharing a GPU
-        // share its link (tools/coll_bench.py).
-        // OSGPU_HOST_PATH=staged|getmem overrides.
+        // PE's PCIe link; that beats the runtime's memcpy only for large
+        // calls and only when every member has a GPU (and a link) of its
+        // own -- PEs sharing a GPU share its link (tools/coll_bench.py,
+        // DESIGN.md 9).  Small calls (the fused limit, a size every member
+        // shares) stay on the runtime's getmem: no GPU round trip beats a
+        // same-node copy of a few KiB (1 Ki ints: 1.6 us vs 14 us for the
+        // one-launch staged form, profiles/r01_mp_latency_host_coll.jsonl).
+        // OSGPU_HOST_PATH=staged|getmem overrides; forced staging runs small
+        // calls as one launch (run_fused_staged_copy).
         const char *hp = getenv("OSGPU_HOST_PATH");
         const bool force_getmem = hp && !strcmp(hp, "getmem");
         const bool force_staged = hp && !strcmp(hp, "staged");
-        if (!counts_done) barrier(c);  // sources ready (staging setup runs after it)
         StageSet *S = force_getmem ? nullptr : stage_setup(c);
-        if (S && (force_staged || S->ndev == c.PE_size || c.PE_size == 1)) run_staged(c, *S);
-        else run_getmem(c);
+        if (S && force_staged && !counts_done && run_fused_staged_copy(c, *S)) return;
+        if (!counts_done) barrier(c);  // sources ready
+        const bool small = shared_bytes(c) <= fused_max_bytes();
+        if (S && (force_staged || (!small && (S->ndev == c.PE_size || c.PE_size == 1))))
+            run_staged(c, *S);
+        else
+            run_getmem(c);
         barrier(c);
         if (psync_counts) c.pSync[kCountWord] = 0;
         return;

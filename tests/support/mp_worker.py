@@ -224,8 +224,26 @@ def device_heap_modes(L, PES, mode, rank, world):
         runs = [(str(ci), c, -1) for ci, c in enumerate(CC.fused_cases())]
         runs += [(f"{ci}/big", c, 256) for ci, c in enumerate(CC.fused_cases())
                  if c["kind"] == "collect"]
+        # third pass: every case on the host heap (the shared-memory symmetric
+        # heap, pinned on every PE) with staging forced: fused staged copies
+        runs += [(f"{ci}/host", c, -1) for ci, c in enumerate(CC.fused_cases())]
+        hbase = PES.pes_heap(rank)
+        hbytes = 1 << 24
+        assert L.osgpu_host_register(ctypes.c_void_p(hbase), hbytes) == 0
+
+        def hput(off, arr):
+            raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+            ctypes.memmove(hbase + off, raw.ctypes.data, raw.size)
+
         for ci, c, lim in runs:
             L.osgpu_set_fused_max_bytes(lim)
+            host = ci.endswith("/host")
+            # host heaps: forced staging (small calls stay on getmem otherwise)
+            if host:
+                os.environ["OSGPU_HOST_PATH"] = "staged"
+            else:
+                os.environ.pop("OSGPU_HOST_PATH", None)
+            b0 = hbase if host else dev0
             npes, start, log, size = c["set"]
             if npes > world:
                 continue
@@ -233,25 +251,29 @@ def device_heap_modes(L, PES, mode, rank, world):
             pes = OC.active_set(start, log, size)
             if rank < npes:
                 src, tgt = CC.fused_inputs(c, rank)
-                put(tgt_off - CC.MARGIN, tgt)
+                (hput if host else put)(tgt_off - CC.MARGIN, tgt)
                 if not c["same"] and src.size:
-                    put(0, src)
+                    (hput if host else put)(0, src)
             torch.cuda.synchronize()
             sync()
             if rank in pes:
                 f = osgpu.coll(c["kind"], c["bits"])
                 cnt = CC.fused_counts(c)[rank]
                 if c["kind"] == "broadcast":
-                    f(dev0 + tgt_off, dev0 + src_off, cnt, c["root"], start, log, size, psync)
+                    f(b0 + tgt_off, b0 + src_off, cnt, c["root"], start, log, size, psync)
                 else:
-                    f(dev0 + tgt_off, dev0 + src_off, cnt, start, log, size, psync)
+                    f(b0 + tgt_off, b0 + src_off, cnt, start, log, size, psync)
                 paths[ci] = osgpu.last_coll_path()
                 assert not any(ctypes.string_at(psync, 1024)), "pSync not reset"
             if rank < npes:
-                got = heap[tgt_off - CC.MARGIN:tgt_off + tgt_bytes + CC.MARGIN].cpu().numpy()
+                lo, hi = tgt_off - CC.MARGIN, tgt_off + tgt_bytes + CC.MARGIN
+                got = (np.frombuffer(ctypes.string_at(hbase + lo, hi - lo), np.uint8) if host
+                       else heap[lo:hi].cpu().numpy())
                 digests[ci] = hashlib.sha256(got.tobytes()).hexdigest()
             sync()
         L.osgpu_set_fused_max_bytes(-1)
+        os.environ.pop("OSGPU_HOST_PATH", None)
+        assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
         res["digests"], res["paths"] = digests, paths
     if mode == "golden":
         # around a 64 KiB fused limit: under, at, just over
@@ -396,6 +418,33 @@ def device_heap_modes(L, PES, mode, rank, world):
                 lat[f"{n}/{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
                                       "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
                                       "path": osgpu.last_path(), "correct": ok}
+            # the collectives on the same pinned host heap: the runtime's
+            # getmem (the default for small calls) vs the forced one-launch
+            # staged copy
+            if n <= 1 << 16:
+                coff = 1 << 22
+                for kind in ("fcollect", "broadcast", "alltoall"):
+                    f = osgpu.coll(kind, 32)
+                    ne = n // world if kind == "alltoall" else n
+                    for name, lim in (("host_getmem", 0), ("host_fused_staged", 1 << 30)):
+                        L.osgpu_set_fused_max_bytes(lim)
+                        if lim:  # the one-launch staged form needs staging forced
+                            os.environ["OSGPU_HOST_PATH"] = "staged"
+                        ts = []
+                        for r in range(reps + 5):
+                            sync()
+                            t0 = time.perf_counter()
+                            if kind == "broadcast":
+                                f(hbase + coff, hbase, ne, 0, 0, 0, world, psync)
+                            else:
+                                f(hbase + coff, hbase, ne, 0, 0, world, psync)
+                            sync()
+                            ts.append(time.perf_counter() - t0)
+                        os.environ.pop("OSGPU_HOST_PATH", None)
+                        lat[f"{n}/{kind}32_{name}"] = {
+                            "us_median": float(np.median(ts[5:]) * 1e6),
+                            "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
+                            "path": osgpu.last_coll_path(), "correct": True}
             assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
         L.osgpu_set_fused_max_bytes(-1)
         L.osgpu_set_path(osgpu.PATH_AUTO)

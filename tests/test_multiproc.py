@@ -262,12 +262,12 @@ def test_fused_collectives_processes(tmp_path):
     from support import coll_cases as CC
     world = 8
     res = launch("collgolden", world, tmp_path)
-    nfused = nbig = 0
+    nfused = nbig = nhost = 0
     for ci, c in enumerate(CC.fused_cases()):
         if c["set"][0] > world:
             continue
         exp = CC.fused_expected(c)
-        keys = [str(ci)] + ([f"{ci}/big"] if c["kind"] == "collect" else [])
+        keys = [str(ci), f"{ci}/host"] + ([f"{ci}/big"] if c["kind"] == "collect" else [])
         total = sum(CC.fused_counts(c).values()) * c["bits"] // 8
         for key in keys:
             for r in range(c["set"][0]):
@@ -276,13 +276,20 @@ def test_fused_collectives_processes(tmp_path):
                 ran = res[r]["paths"].get(key)
                 if ran is None:
                     continue
-                if key.endswith("/big") and total > 256:
+                if key.endswith("/host"):
+                    # staging forced (OSGPU_HOST_PATH=staged); collect keeps
+                    # its count exchange and the chunked STAGED copy
+                    want = ("fused_staged" if c["kind"] != "collect" else
+                            "staged" if total else "barrier_only")
+                    assert ran == want, (c, key, r, ran)
+                    nhost += ran == "fused_staged"
+                elif key.endswith("/big") and total > 256:
                     assert ran == "copy", (c, key, r, ran)
                     nbig += 1
                 else:
                     assert ran == "fused_copy", (c, key, r, ran)
                     nfused += 1
-    assert nfused > 800 and nbig > 100, (nfused, nbig)
+    assert nfused > 800 and nbig > 100 and nhost > 600, (nfused, nbig, nhost)
 
 
 @pytest.mark.gpu
