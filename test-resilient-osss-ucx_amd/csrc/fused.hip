@@ -220,47 +220,6 @@ __device__ __forceinline__ void fused_done(const FusedArgs &a, int &s_go)
     (void) s_go;
 }
 
-// The data-movement collectives' small calls (shmem_collect.cpp): the pieces
-// of my target pulled from every member's source, between the same device
-// barriers.  Segment d: a.seg_bytes[d] bytes from a.src[d] to a.dst[d].
-// Staged form (host heaps): my host source is first copied into my device
-// staging slot by the whole grid, the last workgroup arrives; the segments
-// then read the members' staging slots and write my host target directly.
-__global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
-{
-    __shared__ int s_go;
-    if (a.host_in) {
-        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
-            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
-        if (threadIdx.x == 0)
-            s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
-        __syncthreads();
-        if (!s_go) return;
-    } else if (!fused_arrive(a, s_go)) {
-        return;
-    }
-    const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
-    const size_t stride = (size_t) gridDim.x * kFBlock;
-    for (int d = 0; d < a.nseg; d++) {
-        const char *src = static_cast<const char *>(a.src[d]);
-        char *dst = static_cast<char *>(a.dst[d]);
-        const size_t nb = a.seg_bytes[d];
-        if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0) {
-            const size_t nv = nb / 16;
-            for (size_t j = tid; j < nv; j += stride)
-                store_out(reinterpret_cast<u32x4 *>(dst) + j,
-                          __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src) + j));
-            for (size_t b = nv * 16 + tid; b < nb; b += stride) dst[b] = src[b];
-        } else {
-            for (size_t b = tid; b < nb; b += stride) dst[b] = src[b];
-        }
-    }
-    fused_done(a, s_go);
-}
-
 // Grid-stride copy of one piece at the widest width both ends allow.
 __device__ __forceinline__ void copy_piece(char *dst, const char *src, size_t nb, size_t tid,
                                            size_t stride)
@@ -286,6 +245,36 @@ __device__ __forceinline__ void copy_piece(char *dst, const char *src, size_t nb
         done = nw * 4;
     }
     for (size_t b = done + tid; b < nb; b += stride) dst[b] = src[b];
+}
+
+// The data-movement collectives' small calls (shmem_collect.cpp): the pieces
+// of my target pulled from every member's source, between the same device
+// barriers.  Segment d: a.seg_bytes[d] bytes from a.src[d] to a.dst[d].
+// Staged form (host heaps): my host source is first copied into my device
+// staging slot by the whole grid, the last workgroup arrives; the segments
+// then read the members' staging slots and write my host target directly.
+__global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
+{
+    __shared__ int s_go;
+    if (a.host_in) {
+        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
+            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
+        if (threadIdx.x == 0)
+            s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
+        __syncthreads();
+        if (!s_go) return;
+    } else if (!fused_arrive(a, s_go)) {
+        return;
+    }
+    const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
+    const size_t stride = (size_t) gridDim.x * kFBlock;
+    for (int d = 0; d < a.nseg; d++)
+        copy_piece(static_cast<char *>(a.dst[d]), static_cast<const char *>(a.src[d]),
+                   a.seg_bytes[d], tid, stride);
+    fused_done(a, s_go);
 }
 
 // collect (shmem_collect.cpp, src/shmemc/collect.c:24-69): contributions

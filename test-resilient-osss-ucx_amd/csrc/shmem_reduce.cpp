@@ -317,7 +317,7 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
         fused_wait(c.name, S, st, a.epoch);
     }
     if (trace) {
-        const double tk = 1e6 / 1e8;  // us per tick of the 100 MHz wall clock
+        const double tk = 1e3 / S.rate_khz;  // us per tick of the device wall clock
         fprintf(stderr, "[osgpu fused PE %d epoch %llu] arrive-wait %.2f body %.2f fence %.2f "
                         "ticket+fence %.2f done-wait %.2f us\n", c.me, a.epoch,
                 (trace[1] - trace[0]) * tk, (trace[2] - trace[1]) * tk,
