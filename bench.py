@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--nreduce", type=int, default=64 << 20)
     ap.add_argument("--no-rccl", action="store_true", help="N>1: skip the RCCL runs")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N>1: skip the config-4 (1 Gi, RCCL) and config-5 (host) runs")
+                    help="skip the side measurements (N=1: north star / config 3 "
+                         "kernel rates; N>1: config 4, config 5, collectives, probes)")
     ap.add_argument("--c4-nreduce", type=int, default=1 << 30)
     ap.add_argument("--c5-nreduce", type=int, default=128 << 20)
     ap.add_argument("--deadline", type=float, default=420.0,
@@ -346,10 +347,11 @@ def bench_single(args):
     }
     del a, b, out
     torch.cuda.empty_cache()
-    try:
-        res.update(extra_kernel_rates(L, torch))
-    except Exception as e:  # report, never hide
-        res["extra_kernels"] = {"error": repr(e)}
+    if not args.no_extra:
+        try:
+            res.update(extra_kernel_rates(L, torch))
+        except Exception as e:  # report, never hide
+            res["extra_kernels"] = {"error": repr(e)}
     tr = load_traffic()
     res["roofline"] = {
         "bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

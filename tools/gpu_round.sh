@@ -20,7 +20,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 20 --warmup 5 ;;
     tune)  step tune 300 ./tools/tune_combine ;;
     latency) step latency 300 python tools/latency_probe.py ;;
     mplat) step mplat 400 python tools/mp_latency.py ;;
