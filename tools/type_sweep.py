@@ -41,8 +41,10 @@ bufs = [torch.empty(BYTES, dtype=torch.uint8, device="cuda") for _ in range(9)]
 for b in bufs:
     b.view(torch.float32).uniform_(0.5, 1.5)   # finite, non-NaN bit patterns for every type
 out = bufs[8]
-for K in (2, 8):
-    for t in osgpu.TYPES:
+KS = [int(k) for k in os.environ.get("TS_KS", "2,8").split(",")]
+TS = os.environ.get("TS_TYPES", ",".join(osgpu.TYPES)).split(",")
+for K in KS:
+    for t in TS:
         for op in osgpu.OPS:
             if not osgpu.has_op(t, op):
                 continue
