@@ -389,7 +389,9 @@ def bench_single(args):
 # --------------------------------------------------------------------------
 
 def _log(rank, msg):
-    print(f"[bench rank {rank}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+    # one write per line: ranks share the stream
+    sys.stderr.write(f"[bench rank {rank}] {time.strftime('%H:%M:%S')} {msg}\n")
+    sys.stderr.flush()
 
 
 def _sample_parity(rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15, t="double"):
