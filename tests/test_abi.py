@@ -149,19 +149,21 @@ def test_zero_length_collective_only_synchronises(lib):
         assert [a - b for a, b in zip(after, before)] == [2, 2, 2, 2]
 
 
-def test_fails_loudly_without_gpu():
-    """Host-memory call on a machine with no GPU: abort with a message, never
-    a CPU result."""
+@pytest.mark.parametrize("call", ["tm.run('int', 'sum', 1024, 0, 8)",
+                                  "tm.run_coll('fcollect', 32, 1024, 0, 8)"])
+def test_fails_loudly_without_gpu(call):
+    """Host-memory call on a machine with no GPU (a reduction, and a
+    data-movement collective): abort with a message, never a CPU result."""
     code = (
         "import sys, ctypes; sys.path[:0]=[%r, %r, %r]\n"
         "import numpy as np\n"
         "from support import team as T\n"
         "tm = T.Team(2, 4096, device=False)\n"
         "tm.write(0, 0, np.arange(8, dtype=np.int32)); tm.write(1, 0, np.arange(8, dtype=np.int32))\n"
-        "tm.run('int', 'sum', 1024, 0, 8)\n"
+        "%s\n"
         "print('COMPUTED')\n"
     ) % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "test-resilient-osss-ucx_amd"),
-         os.path.join(ROOT, "oracle"))
+         os.path.join(ROOT, "oracle"), call)
     env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                        timeout=300, env=env)
