@@ -28,10 +28,14 @@
 //   STAGED  host arguments, every member on a GPU of its own: H2D my source
 //           -> copy kernel over every PE's IPC-mapped device staging -> D2H
 //           of my target, chunked (each PE's PCIe link carries its bytes);
-//   GETMEM  host arguments when members share a GPU (and so its PCIe link)
-//           or staging cannot be mapped: the reference's own linear
-//           algorithm over the runtime's shmem_getmem -- pure byte movement,
-//           which the runtime's memcpy does at memory speed.
+//   GETMEM  host arguments of small calls, or when members share a GPU (and
+//           so its PCIe link), or when staging cannot be mapped: the
+//           reference's own linear algorithm over the runtime's shmem_getmem
+//           -- pure byte movement, which the runtime's memcpy does at memory
+//           speed.
+//   FUSED   small calls with every member its own process: ONE launch whose
+//           barriers are device flags (fused.hip) -- device heaps always,
+//           host heaps when staging is forced (OSGPU_HOST_PATH=staged).
 //
 // collect needs every PE's nelems before any byte moves.  On device heaps
 // the counts ride on the device-side arrival of a fused launch (fused.hip
