@@ -702,10 +702,12 @@ def bench_multi(args):
         res["ms_per_step"] = t / args.steps * 1e3
         res["config"]["path"] = "p2p-team (exact owner-computes kernel over IPC-mapped HBM, xGMI)"
         res["config"]["algbw_GiBs"] = n * 8 * args.steps / t / GIB
-        # the exchange is link-bound: per step every GPU pulls n*8/P bytes
-        # from each of its P-1 peers and pushes as many back, one xGMI link
-        # per peer (the traffic of a reduce-scatter + all-gather)
-        per_dir = (world - 1) * (n * 8 // world) * args.steps / t / 1e9
+        # the exchange is link-bound: per step GPU g reads shard g of each
+        # peer's source (n*8/P bytes per peer) and each peer h writes shard h
+        # of g's target: 2*(P-1)*n*8/P bytes arrive at every GPU (and as many
+        # leave), 2*n*8/P per link and direction -- the traffic of a
+        # reduce-scatter + all-gather over a fully connected fabric
+        per_dir = 2 * (world - 1) * (n * 8 // world) * args.steps / t / 1e9
         peak = (world - 1) * XGMI_LINK_GBS
         agg = args.steps * B / t / 1e9
         res["hbm_aggregate"] = {"GBs": agg, "peak_GBs": world * HBM_PEAK_GBS,
@@ -717,8 +719,10 @@ def bench_multi(args):
             "frac": per_dir / peak, "traffic": None,
             "kernel": f"osgpu::team_vec_kernel<double, SUM, {world}>",
             "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
-                     f"second (it sends as many); peak = {world - 1} x {XGMI_LINK_GBS} GB/s per "
-                     f"direction (MI355X xGMI, 153.6 GB/s bidirectional per link)")}
+                     f"second: the shard reads from every peer plus every peer's writes of its "
+                     f"shard into this GPU's target (it sends as many); peak = {world - 1} x "
+                     f"{XGMI_LINK_GBS} GB/s per direction (MI355X xGMI, 153.6 GB/s "
+                     f"bidirectional per link)")}
         if ndev < world:  # a rehearsal with ranks sharing GPUs: no xGMI involved
             res["roofline"]["frac"] = None
             res["roofline"]["note"] += "; ranks share a GPU here, so no link is used"
@@ -740,7 +744,7 @@ def bench_multi(args):
                                 "ms_per_step": tp / args.steps * 1e3,
                                 "algbw_GiBs": n * 8 * args.steps / tp / GIB,
                                 "xgmi_GBs_per_gpu_per_direction":
-                                    (world - 1) * (n * 8 // world) * args.steps / tp / 1e9,
+                                    2 * (world - 1) * (n * 8 // world) * args.steps / tp / 1e9,
                                 "parity_sample": _sample_parity(rank, world, src, tgt, n, "sum",
                                                                 dist),
                                 "full_target_identical_to_pull_all_ranks":
