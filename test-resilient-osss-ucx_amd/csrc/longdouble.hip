@@ -200,21 +200,39 @@ struct LdTeam {
     unsigned char *dst[kMaxTeam];
 };
 
-// owner-computes form (team.hip): every PE's own fold order, P^2 soft ops
-template <int OP>
-__global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, int P, size_t n)
+// owner-computes form (team.hip): every PE's own fold order, P^2 soft ops;
+// P is a template parameter so the P inputs stay in registers
+template <int OP, int P>
+__global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
 {
     const size_t stride = (size_t) gridDim.x * blockDim.x;
     for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        X80 x[kMaxTeam];
+        X80 x[P];
+#pragma unroll
         for (int p = 0; p < P; p++) x[p] = load(a.src[p] + 16 * i);
+#pragma unroll
         for (int q = 0; q < P; q++) {
             X80 acc = x[q];
+#pragma unroll
             for (int j = 0; j < P; j++)
                 if (j != q) acc = apply<OP>(acc, x[j]);
             store(a.dst[q] + 16 * i, acc);
         }
     }
+}
+
+template <int OP>
+hipError_t ld_team_launch(int P, const LdTeam &a, size_t n, unsigned blocks, hipStream_t s)
+{
+    switch (P) {
+#define LDT(PP)                                                                \
+    case PP:                                                                   \
+        hipLaunchKernelGGL((ld_team_kernel<OP, PP>), dim3(blocks), dim3(256), 0, s, a, n); \
+        return hipGetLastError();
+        LDT(2) LDT(3) LDT(4) LDT(5) LDT(6) LDT(7) LDT(8)
+#undef LDT
+    }
+    return hipErrorInvalidValue;
 }
 
 }  // namespace x87
@@ -232,13 +250,12 @@ hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *
     size_t blocks = (n + 255) / 256;
     blocks = blocks > 16384 ? 16384 : (blocks ? blocks : 1);
     switch (op) {
-    case 0: hipLaunchKernelGGL(x87::ld_team_kernel<0>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
-    case 1: hipLaunchKernelGGL(x87::ld_team_kernel<1>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
-    case 5: hipLaunchKernelGGL(x87::ld_team_kernel<5>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
-    case 6: hipLaunchKernelGGL(x87::ld_team_kernel<6>, dim3((unsigned) blocks), dim3(256), 0, s, a, P, n); break;
-    default: return hipErrorInvalidValue;
+    case 0: return x87::ld_team_launch<0>(P, a, n, (unsigned) blocks, s);
+    case 1: return x87::ld_team_launch<1>(P, a, n, (unsigned) blocks, s);
+    case 5: return x87::ld_team_launch<5>(P, a, n, (unsigned) blocks, s);
+    case 6: return x87::ld_team_launch<6>(P, a, n, (unsigned) blocks, s);
     }
-    return hipGetLastError();
+    return hipErrorInvalidValue;
 }
 
 }  // namespace osgpu
