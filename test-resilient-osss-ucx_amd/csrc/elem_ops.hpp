@@ -76,7 +76,12 @@ __device__ __forceinline__ float copysign_(float m, float s)
 // x=(a*c-b*d)*inf, y=inf*(a*d+b*c).  Reached only when the inline product
 // has a NaN part, so it lives off the fast path.
 template <typename F>
-__device__ __attribute__((noinline)) void mulc3(F a, F b, F c, F d, F *xr, F *yr)
+struct CPair {
+    F x, y;
+};
+// returned by value (in registers): no stack frame on the fast path's kernels
+template <typename F>
+__device__ __attribute__((noinline)) CPair<F> mulc3(F a, F b, F c, F d)
 {
     const F one = 1, zero = 0, inf = __builtin_huge_val();
     F ac = mul(a, c), bd = mul(b, d), ad = mul(a, d), bc = mul(c, b);
@@ -109,8 +114,7 @@ __device__ __attribute__((noinline)) void mulc3(F a, F b, F c, F d, F *xr, F *yr
             y = mul(inf, add(mul(a, d), mul(b, c)));
         }
     }
-    *xr = x;
-    *yr = y;
+    return CPair<F>{x, y};
 }
 
 // --------------------------------------------------------------- functors
@@ -176,7 +180,11 @@ __device__ __forceinline__ C cmul(C p, C q)
     F a = p.re, b = p.im, c = q.re, d = q.im;
     F x = a * c - b * d;   // inline fast path; any NaN part -> libgcc path
     F y = a * d + b * c;
-    if (__builtin_expect(x != x || y != y, 0)) mulc3<F>(a, b, c, d, &x, &y);
+    if (__builtin_expect(x != x || y != y, 0)) {
+        const CPair<F> r = mulc3<F>(a, b, c, d);
+        x = r.x;
+        y = r.y;
+    }
     return C{x, y};
 }
 template <> struct Elem<cdouble, OP_PROD> {
