@@ -171,6 +171,11 @@ void run_team_push(const Call &c, const std::vector<const void *> &srcs,
     t_last_path = OSGPU_RAN_TEAM_PUSH;
     DBG("%s PE %d: team push, %lld chunks of %lld", c.name, c.me, nchunks, C);
     entry_sync(c.name, st);
+    // The inboxes are the staging areas of this active set, whose out slots
+    // a member may still be draining into its host target after a STAGED or
+    // fused-staged call it has not yet returned from: no member scatters
+    // before every member has entered this call.
+    barrier(c);
     std::vector<osgpu::CopySeg> segs;
     std::vector<const void *> sp(P);
     std::vector<void *> dp(P);
@@ -327,7 +332,18 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     if (!fused_check(c.name, S, a.epoch, !overlap)) t_last_path = OSGPU_RAN_FUSED_FAILED;
 }
 
-bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *mult)
+// RCCL's arithmetic for a (type, op), or false.
+//  * integer sum/prod/min/max: order-independent (wrapping ring, lattice),
+//    so ncclAllReduce is bit-exact -- allowed on the automatic path;
+//  * FP / complex sum and prod: RCCL folds in its own order, identical on
+//    every PE, where the reference folds in a per-PE order
+//    (src/reductions.c:79-111): within tolerance only, so only when the
+//    caller forces OSGPU_PATH_RCCL (`fp_ok`);
+//  * FP min/max: never.  The reference's `a<b?a:b` / `a>b?a:b`
+//    (src/shmemu/miscops.c:80-90) resolves NaN and signed-zero ties by fold
+//    position; RCCL's min/max do not follow it.
+bool rccl_types(int type, int op, bool fp_ok, ncclDataType_t *dt, ncclRedOp_t *rop,
+                size_t *mult)
 {
     *mult = 1;
     switch (op) {
@@ -337,18 +353,19 @@ bool rccl_types(int type, int op, ncclDataType_t *dt, ncclRedOp_t *rop, size_t *
     case OSGPU_OP_MIN: *rop = ncclMin; break;
     default: return false;
     }
+    const bool arith = op == OSGPU_OP_SUM || op == OSGPU_OP_PROD;
     switch (type) {
     case OSGPU_T_INT: *dt = ncclInt32; return true;
     case OSGPU_T_LONG: case OSGPU_T_LONGLONG: *dt = ncclInt64; return true;
-    case OSGPU_T_FLOAT: *dt = ncclFloat32; return true;
-    case OSGPU_T_DOUBLE: *dt = ncclFloat64; return true;
-    case OSGPU_T_COMPLEXF: *dt = ncclFloat32; *mult = 2; return op == OSGPU_OP_SUM;
-    case OSGPU_T_COMPLEXD: *dt = ncclFloat64; *mult = 2; return op == OSGPU_OP_SUM;
+    case OSGPU_T_FLOAT: *dt = ncclFloat32; return fp_ok && arith;
+    case OSGPU_T_DOUBLE: *dt = ncclFloat64; return fp_ok && arith;
+    case OSGPU_T_COMPLEXF: *dt = ncclFloat32; *mult = 2; return fp_ok && op == OSGPU_OP_SUM;
+    case OSGPU_T_COMPLEXD: *dt = ncclFloat64; *mult = 2; return fp_ok && op == OSGPU_OP_SUM;
     }
     return false;
 }
 
-bool rccl_usable(const Call &c)
+bool rccl_usable(const Call &c, bool forced)
 {
     ncclDataType_t dt;
     ncclRedOp_t rop;
@@ -357,7 +374,7 @@ bool rccl_usable(const Call &c)
     // which every PE of the parent must call -- OpenSHMEM forbids
     // non-members from calling a collective on an active set
     return g_rccl.world && c.PE_start == 0 && c.step == 1 && c.PE_size == g_rccl.npes &&
-           c.me == g_rccl.me && rccl_types(c.type, c.op, &dt, &rop, &mult);
+           c.me == g_rccl.me && rccl_types(c.type, c.op, forced, &dt, &rop, &mult);
 }
 
 void run_rccl(const Call &c)
@@ -365,7 +382,7 @@ void run_rccl(const Call &c)
     ncclDataType_t dt;
     ncclRedOp_t rop;
     size_t mult;
-    rccl_types(c.type, c.op, &dt, &rop, &mult);
+    rccl_types(c.type, c.op, true, &dt, &rop, &mult);
     t_last_path = OSGPU_RAN_RCCL;
     hipStream_t st = pe_stream(c.name, c.me);
     entry_sync(c.name);
@@ -595,8 +612,13 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     std::vector<void *> dsts;
     int idx = -1;
     SyncSet *S = nullptr;
-    if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_P2P) &&
-        (idx = team_ptrs(c, srcs, dsts)) >= 0) {
+    // RCCL only where its result is the reference's: integer (type, op)s on
+    // the automatic path when no device heap is registered; FP sum/prod only
+    // when the caller forces OSGPU_PATH_RCCL (tolerance, not bit-exact); FP
+    // min/max never (they take the exact kernels even when RCCL is forced).
+    if (mode == OSGPU_PATH_RCCL && rccl_usable(c, true)) {
+        run_rccl(c);
+    } else if (mode != OSGPU_PATH_PULL && (idx = team_ptrs(c, srcs, dsts)) >= 0) {
         StageSet *G = nullptr;
         if (fused_eligible(c, true) && (S = sync_setup(c)))
             run_fused(c, *S, srcs, dsts, true);
@@ -604,20 +626,21 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
             run_team_push(c, srcs, dsts, idx, *G);
         else
             run_team(c, srcs, dsts, idx);
-    } else if (mode != OSGPU_PATH_RCCL && member_sources(c, srcs)) {
+    } else if (member_sources(c, srcs)) {
         if (fused_eligible(c, false) && (S = sync_setup(c))) {
             run_fused(c, *S, srcs, dsts, false);
         } else {
             p2p_sources(c, srcs);
             run_p2p(c, srcs);
         }
-    } else if ((mode == OSGPU_PATH_AUTO || mode == OSGPU_PATH_RCCL) && rccl_usable(c)) {
+    } else if (mode == OSGPU_PATH_AUTO && rccl_usable(c, false)) {
         run_rccl(c);
     } else {
         fatal(name,
-              "device-resident arguments need either every active PE's device heap "
-              "registered (osgpu_heap_register) or an RCCL communicator covering the "
-              "active set with a supported type/op (path mode %d)",
+              "device-resident arguments need every active PE's device heap registered "
+              "(osgpu_heap_create / osgpu_heap_register), or -- integer types only, or FP "
+              "sum/prod under OSGPU_PATH_RCCL -- an RCCL communicator over the whole job "
+              "(path mode %d)",
               mode);
     }
     if (cur != dt) HIPCHK(name, hipSetDevice(cur));

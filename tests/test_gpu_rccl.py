@@ -61,7 +61,11 @@ def test_rccl_one_rank_is_identity(rccl_team, t, op, n):
     tm.write(0, 0, src)
     tm.fill(0, toff, nb, 0xA5)
     tm.run(t, op, toff, 0, n)
-    assert tm.last_paths[0] == "rccl"
+    # FP min/max never go to RCCL, even forced: RCCL does not resolve NaN and
+    # signed-zero ties like src/shmemu/miscops.c:80-90, so the exact kernels
+    # run (here the pull form over the one registered heap)
+    fp_minmax = t in ("float", "double") and op in ("max", "min")
+    assert tm.last_paths[0] == ("pull" if fp_minmax else "rccl")
     np.testing.assert_array_equal(tm.read(0, toff, nb), src)
     np.testing.assert_array_equal(tm.read(0, 0, nb), src)  # source untouched
 
