@@ -1,0 +1,511 @@
+// heap.cpp -- the device symmetric heap as ONE contiguous virtual range per
+// PE, mapped into every member of the job (osgpu_heap_create).
+//
+// The reference's symmetric heap is one contiguous region per PE
+// (register_symmetric_heap, src/shmemc/ucx-init.c:174-213) and a symmetric
+// object of any size is found on PE p at heap_base[p] + offset
+// (translate_address, src/shmemc/comms.c:89-105).  HIP IPC
+// (hipIpcGetMemHandle) cannot give that on this platform: an exported
+// allocation of 2 GiB or more hangs the importer, so
+// objects >= 2 GiB could not be symmetric across processes.
+//
+// Here every PE builds its heap with the virtual memory API instead:
+//   * reserve one virtual range of the heap's size (hipMemAddressReserve);
+//   * back it with physical chunks of at most OSGPU_HEAP_CHUNK_BYTES
+//     (default 1 GiB, a multiple of the allocation granularity), each a
+//     hipMemCreate allocation exportable as a dmabuf file descriptor;
+//   * map the chunks back to back: the PE's own view is contiguous;
+//   * hand the chunk descriptors to every member in another process over a
+//     Unix-domain socket (SCM_RIGHTS; the socket's name and the chunk layout
+//     travel through spare pSync words and the runtime's shmem_getmem, like
+//     the staging setup in runtime.cpp);
+//   * each member imports the chunks and maps them back to back into ONE
+//     virtual range of its own: its view of the peer's heap is contiguous too.
+// Members that are threads of one process share the PE's range directly.
+// The result is registered as segment 0 of every member's heap, so every
+// path (team, pull, fused) sees base + offset for objects of any size.
+#include <hip/hip_runtime_api.h>
+
+#include <errno.h>
+#include <poll.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/osgpu_reduce.h"
+#include "runtime.hpp"
+
+namespace osgpu {
+namespace rt {
+
+namespace {
+
+constexpr int kHeapPsync = 16;       // pSync[16..] during setup only (cf. runtime.cpp)
+constexpr int kFdBatch = 64;         // descriptors per SCM_RIGHTS message
+constexpr int kSetupTimeoutMs = 120000;
+
+struct Mapping {                     // one heap as mapped in this process
+    int pe = -1;
+    int device = -1;                 // this process's device whose HBM backs it, or -1
+    char *base = nullptr;
+    size_t bytes = 0;                // reserved bytes
+    std::vector<hipMemGenericAllocationHandle_t> h;
+    std::vector<size_t> len;         // chunk lengths
+    size_t nmapped = 0;              // chunks mapped so far
+};
+
+struct Heap {                        // the heap a PE created, with its imports
+    int pe = -1;
+    Mapping own;
+    std::vector<Mapping> peers;      // members in other processes
+};
+
+std::mutex g_hmu;
+std::vector<Heap *> g_heaps;
+
+// what a PE publishes in pSync[16..] during osgpu_heap_create
+struct HeapMsg {
+    long pid, nonce, bytes, chunk, raw_ptr, status, device, pad;
+};
+static_assert(sizeof(HeapMsg) <= (64 - kHeapPsync) * sizeof(long), "pSync room");
+
+void sock_name(long pid, long nonce, sockaddr_un *a, socklen_t *len)
+{
+    memset(a, 0, sizeof(*a));
+    a->sun_family = AF_UNIX;
+    // abstract namespace: nothing on the file system to clean up
+    const int n = snprintf(a->sun_path + 1, sizeof(a->sun_path) - 1, "osgpu-heap-%ld-%ld", pid,
+                           nonce);
+    *len = (socklen_t) (offsetof(sockaddr_un, sun_path) + 1 + n);
+}
+
+bool write_all(int fd, const void *p, size_t n)
+{
+    const char *c = (const char *) p;
+    while (n) {
+        const ssize_t w = send(fd, c, n, MSG_NOSIGNAL);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) return false;
+        c += w;
+        n -= (size_t) w;
+    }
+    return true;
+}
+
+// descriptors in batches of kFdBatch, each batch riding on one byte
+bool send_fds(int s, const std::vector<int> &fds)
+{
+    const unsigned long long n = fds.size();
+    if (!write_all(s, &n, sizeof(n))) return false;
+    for (size_t i = 0; i < fds.size(); i += kFdBatch) {
+        const int m = (int) std::min(fds.size() - i, (size_t) kFdBatch);
+        char byte = 'F';
+        iovec iov = {&byte, 1};
+        std::vector<char> ctl(CMSG_SPACE(sizeof(int) * m));
+        msghdr msg;
+        memset(&msg, 0, sizeof(msg));
+        msg.msg_iov = &iov;
+        msg.msg_iovlen = 1;
+        msg.msg_control = ctl.data();
+        msg.msg_controllen = ctl.size();
+        cmsghdr *cm = CMSG_FIRSTHDR(&msg);
+        cm->cmsg_level = SOL_SOCKET;
+        cm->cmsg_type = SCM_RIGHTS;
+        cm->cmsg_len = CMSG_LEN(sizeof(int) * m);
+        memcpy(CMSG_DATA(cm), fds.data() + i, sizeof(int) * m);
+        ssize_t w;
+        do w = sendmsg(s, &msg, MSG_NOSIGNAL); while (w < 0 && errno == EINTR);
+        if (w != 1) return false;
+    }
+    return true;
+}
+
+bool read_all(int fd, void *p, size_t n)
+{
+    char *c = (char *) p;
+    while (n) {
+        const ssize_t r = recv(fd, c, n, 0);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        c += r;
+        n -= (size_t) r;
+    }
+    return true;
+}
+
+bool recv_fds(int s, std::vector<int> &fds)
+{
+    unsigned long long n = 0;
+    if (!read_all(s, &n, sizeof(n)) || n > (1u << 20)) return false;
+    while (fds.size() < n) {
+        const int m = (int) std::min<unsigned long long>(n - fds.size(), kFdBatch);
+        char byte = 0;
+        iovec iov = {&byte, 1};
+        std::vector<char> ctl(CMSG_SPACE(sizeof(int) * m));
+        msghdr msg;
+        memset(&msg, 0, sizeof(msg));
+        msg.msg_iov = &iov;
+        msg.msg_iovlen = 1;
+        msg.msg_control = ctl.data();
+        msg.msg_controllen = ctl.size();
+        ssize_t r;
+        do r = recvmsg(s, &msg, MSG_CMSG_CLOEXEC); while (r < 0 && errno == EINTR);
+        if (r != 1) return false;
+        cmsghdr *cm = CMSG_FIRSTHDR(&msg);
+        if (!cm || cm->cmsg_type != SCM_RIGHTS) return false;
+        const int got = (int) ((cm->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+        const size_t at = fds.size();
+        fds.resize(at + got);
+        memcpy(fds.data() + at, CMSG_DATA(cm), sizeof(int) * got);
+    }
+    return true;
+}
+
+hipMemAllocationProp chunk_prop(int dev)
+{
+    hipMemAllocationProp p;
+    memset(&p, 0, sizeof(p));
+    p.type = hipMemAllocationTypePinned;
+    p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    p.location.type = hipMemLocationTypeDevice;
+    p.location.id = dev;
+    return p;
+}
+
+// read-write access from this process's current device (required); for the
+// PE's own heap (`own`) also from every other visible device that can reach
+// it as a peer -- PEs that are threads of this process on other GPUs use
+// the range directly (best effort)
+bool grant_access(char *base, size_t bytes, int dev, bool own)
+{
+    hipMemAccessDesc d;
+    memset(&d, 0, sizeof(d));
+    d.location.type = hipMemLocationTypeDevice;
+    d.location.id = dev;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    if (hipMemSetAccess(base, bytes, &d, 1) != hipSuccess) return false;
+    int ndev = 0;
+    if (!own || hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    for (int o = 0; o < ndev; o++) {
+        int can = 0;
+        if (o == dev || hipDeviceCanAccessPeer(&can, o, dev) != hipSuccess || !can) continue;
+        d.location.id = o;
+        if (hipMemSetAccess(base, bytes, &d, 1) != hipSuccess) (void) hipGetLastError();
+    }
+    (void) hipGetLastError();
+    return true;
+}
+
+void unmap(Mapping &m)
+{
+    size_t off = 0;
+    for (size_t k = 0; k < m.nmapped; off += m.len[k], k++)
+        (void) hipMemUnmap(m.base + off, m.len[k]);
+    for (auto h : m.h) (void) hipMemRelease(h);
+    if (m.base) (void) hipMemAddressFree(m.base, m.bytes);
+    (void) hipGetLastError();
+    m = Mapping();
+}
+
+// chunk lengths of a heap of `bytes` (a multiple of the granularity) in
+// chunks of `chunk`
+std::vector<size_t> chunk_lens(size_t bytes, size_t chunk)
+{
+    std::vector<size_t> v;
+    for (size_t off = 0; off < bytes; off += chunk) v.push_back(std::min(chunk, bytes - off));
+    return v;
+}
+
+// reserve one range and map `h` (lengths `len`) back to back into it
+bool map_chunks(Mapping &m, size_t align, int dev, bool own)
+{
+    void *va = nullptr;
+    if (hipMemAddressReserve(&va, m.bytes, align, nullptr, 0) != hipSuccess) return false;
+    m.base = (char *) va;
+    size_t off = 0;
+    for (size_t k = 0; k < m.h.size(); off += m.len[k], k++) {
+        if (hipMemMap(m.base + off, m.len[k], 0, m.h[k], 0) != hipSuccess) return false;
+        m.nmapped = k + 1;
+    }
+    return grant_access(m.base, m.bytes, dev, own);
+}
+
+size_t heap_chunk_bytes(size_t gran)
+{
+    const char *e = getenv("OSGPU_HEAP_CHUNK_BYTES");
+    size_t c = e ? strtoull(e, nullptr, 0) : 0;
+    if (!c) c = (size_t) 1 << 30;
+    c = (c + gran - 1) / gran * gran;
+    return c;
+}
+
+}  // namespace
+
+// Inside a heap made by osgpu_heap_create (the PE's own range or a member's
+// mapped into this process)?  *dev: the local device backing it, -1 for a
+// member's heap in another process.
+bool heap_created_range(const void *p, size_t n, int *dev)
+{
+    std::lock_guard<std::mutex> lk(g_hmu);
+    const char *c = (const char *) p;
+    for (Heap *h : g_heaps) {
+        if (c >= h->own.base && c + n <= h->own.base + h->own.bytes) {
+            if (dev) *dev = h->own.device;
+            return true;
+        }
+        for (const Mapping &m : h->peers)
+            if (c >= m.base && c + n <= m.base + m.bytes) {
+                if (dev) *dev = -1;
+                return true;
+            }
+    }
+    return false;
+}
+
+}  // namespace rt
+}  // namespace osgpu
+
+using namespace osgpu::rt;
+
+extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, int PE_size,
+                                 long *pSync, void **base_out)
+{
+    const char *where = "osgpu_heap_create";
+    if (!bytes || !pSync || !base_out || PE_size < 1) {
+        set_err("%s: bad arguments", where);
+        return OSGPU_EINVAL;
+    }
+    Coll c = make_coll(where, PE_start, logPE_stride, PE_size, pSync);
+    if (PE_size > 1 && !c.ops.getmem) {
+        set_err("%s: the PE runtime has no shmem_getmem", where);
+        return OSGPU_ENOPE;
+    }
+    const int idx = c.index_of(c.me);
+    if (idx < 0) {
+        set_err("%s: PE %d is not in the active set", where, c.me);
+        return OSGPU_EINVAL;
+    }
+    int dev = 0;
+    HIPCHK(where, hipGetDevice(&dev));
+    Heap *H = new Heap();
+    H->pe = c.me;
+    bool ok = true;
+    size_t gran = 0;
+    hipMemAllocationProp prop = chunk_prop(dev);
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) !=
+            hipSuccess ||
+        !gran) {
+        (void) hipGetLastError();
+        gran = (size_t) 2 << 20;
+    }
+    const size_t total = (bytes + gran - 1) / gran * gran;
+    const size_t chunk = std::min(heap_chunk_bytes(gran), total);
+    std::vector<int> fds;
+    H->own.pe = c.me;
+    H->own.device = dev;
+    H->own.bytes = total;
+    H->own.len = chunk_lens(total, chunk);
+    for (size_t k = 0; ok && k < H->own.len.size(); k++) {
+        hipMemGenericAllocationHandle_t h;
+        if (hipMemCreate(&h, H->own.len[k], &prop, 0) != hipSuccess) {
+            set_err("%s: hipMemCreate(%zu B) failed", where, H->own.len[k]);
+            ok = false;
+            break;
+        }
+        H->own.h.push_back(h);
+        int fd = -1;
+        if (hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0) !=
+                hipSuccess ||
+            fd < 0) {
+            set_err("%s: hipMemExportToShareableHandle failed", where);
+            ok = false;
+            break;
+        }
+        fds.push_back(fd);
+    }
+    if (ok && !map_chunks(H->own, gran, dev, true)) {
+        set_err("%s: mapping the heap failed", where);
+        ok = false;
+    }
+    (void) hipGetLastError();
+
+    // listening socket for the members in other processes
+    static std::atomic<long> nonce_ctr{0};
+    const long nonce = ((long) time(nullptr) << 20) ^ (nonce_ctr.fetch_add(1) + 1);
+    int lfd = ok ? socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0) : -1;
+    if (ok) {
+        sockaddr_un a;
+        socklen_t al;
+        sock_name((long) getpid(), nonce, &a, &al);
+        if (lfd < 0 || bind(lfd, (sockaddr *) &a, al) != 0 || listen(lfd, 64) != 0) {
+            set_err("%s: unix socket: %s", where, strerror(errno));
+            ok = false;
+        }
+    }
+    HeapMsg *mine = reinterpret_cast<HeapMsg *>(pSync + kHeapPsync);
+    memset(mine, 0, sizeof(*mine));
+    mine->pid = (long) getpid();
+    mine->nonce = nonce;
+    mine->bytes = ok ? (long) total : -1;
+    mine->chunk = (long) chunk;
+    mine->raw_ptr = (long) (uintptr_t) H->own.base;
+    mine->device = dev;
+    barrier(c);
+
+    // everyone's layout; how many members from other processes will connect
+    std::vector<HeapMsg> msg(PE_size);
+    for (int i = 0; i < PE_size; i++) {
+        const int pe = c.pe_at(i);
+        if (pe == c.me) msg[i] = *mine;
+        else c.ops.getmem(&msg[i], mine, sizeof(HeapMsg), pe);
+        if (msg[i].bytes <= 0) ok = false;
+    }
+    int expected = 0;
+    for (int i = 0; i < PE_size; i++)
+        if (c.pe_at(i) != c.me && msg[i].pid != (long) getpid()) expected++;
+    std::atomic<int> served{0};
+    std::thread server;
+    if (lfd >= 0 && expected > 0 && mine->bytes > 0) {
+        server = std::thread([&, lfd, expected] {
+            for (int k = 0; k < expected; k++) {
+                pollfd p = {lfd, POLLIN, 0};
+                if (poll(&p, 1, kSetupTimeoutMs) <= 0) return;
+                const int s = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+                if (s < 0) return;
+                if (send_fds(s, fds)) {
+                    char ack;
+                    (void) read_all(s, &ack, 1);  // the importer has its copies
+                    served.fetch_add(1);
+                }
+                close(s);
+            }
+        });
+    }
+    // import every member's heap (same process: its own range)
+    std::vector<char *> base(PE_size, nullptr);
+    for (int i = 0; i < PE_size && ok; i++) {
+        const int pe = c.pe_at(i);
+        if (pe == c.me) {
+            base[i] = H->own.base;
+            continue;
+        }
+        if (msg[i].pid == (long) getpid()) {
+            base[i] = (char *) (uintptr_t) msg[i].raw_ptr;
+            continue;
+        }
+        const int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        sockaddr_un a;
+        socklen_t al;
+        sock_name(msg[i].pid, msg[i].nonce, &a, &al);
+        std::vector<int> pf;
+        bool got = s >= 0 && connect(s, (sockaddr *) &a, al) == 0 && recv_fds(s, pf);
+        Mapping m;
+        m.pe = pe;
+        m.bytes = (size_t) msg[i].bytes;
+        m.len = chunk_lens(m.bytes, (size_t) msg[i].chunk);
+        got = got && pf.size() == m.len.size();
+        for (size_t k = 0; got && k < pf.size(); k++) {
+            hipMemGenericAllocationHandle_t h;
+            if (hipMemImportFromShareableHandle(&h, (void *) (uintptr_t) pf[k],
+                                                hipMemHandleTypePosixFileDescriptor) !=
+                hipSuccess) {
+                set_err("%s: importing PE %d's heap chunk %zu failed", where, pe, k);
+                got = false;
+                break;
+            }
+            m.h.push_back(h);
+        }
+        for (int fd : pf) close(fd);
+        if (s >= 0) {
+            const char ack = 'A';
+            (void) write_all(s, &ack, 1);
+            close(s);
+        }
+        if (got && !map_chunks(m, gran, dev, false)) {
+            set_err("%s: mapping PE %d's heap failed", where, pe);
+            got = false;
+        }
+        (void) hipGetLastError();
+        if (!got) {
+            if (pf.size() != m.len.size())
+                set_err("%s: %zu of %zu chunk descriptors from PE %d", where, pf.size(),
+                        m.len.size(), pe);
+            unmap(m);
+            ok = false;
+            break;
+        }
+        base[i] = m.base;
+        H->peers.push_back(m);
+    }
+    if (server.joinable()) server.join();
+    if (served.load() != expected && mine->bytes > 0) ok = false;
+    if (lfd >= 0) close(lfd);
+    for (int fd : fds) close(fd);
+
+    // every member's verdict
+    mine->status = ok ? 1 : 2;
+    barrier(c);
+    bool all_ok = ok;
+    for (int i = 0; i < PE_size; i++) {
+        const int pe = c.pe_at(i);
+        if (pe == c.me) continue;
+        long st = 0;
+        c.ops.getmem(&st, &mine->status, sizeof(long), pe);
+        all_ok = all_ok && st == 1;
+    }
+    barrier(c);
+    memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
+    if (!all_ok) {
+        for (Mapping &m : H->peers) unmap(m);
+        unmap(H->own);
+        delete H;
+        if (ok) set_err("%s: another member failed to create or map its heap", where);
+        return OSGPU_EPEER;
+    }
+    for (int i = 0; i < PE_size; i++)
+        osgpu_heap_register_segment(c.pe_at(i), 0, base[i], (size_t) msg[i].bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_hmu);
+        g_heaps.push_back(H);
+    }
+    *base_out = H->own.base;
+    DBG("%s PE %d: heap %zu B at %p (%zu chunks), %d members", where, c.me, total,
+        (void *) H->own.base, H->own.len.size(), PE_size);
+    return OSGPU_OK;
+}
+
+extern "C" int osgpu_heap_destroy(void *base)
+{
+    Heap *H = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_hmu);
+        for (size_t i = 0; i < g_heaps.size(); i++)
+            if (g_heaps[i]->own.base == (char *) base) {
+                H = g_heaps[i];
+                g_heaps.erase(g_heaps.begin() + (long) i);
+                break;
+            }
+    }
+    if (!H) {
+        set_err("osgpu_heap_destroy: %p is not a heap made by osgpu_heap_create", base);
+        return OSGPU_EINVAL;
+    }
+    (void) hipDeviceSynchronize();
+    // forget the registrations that point into these ranges
+    for (const Mapping &m : H->peers) osgpu_heap_unregister(m.pe);
+    osgpu_heap_unregister(H->pe);
+    for (Mapping &m : H->peers) unmap(m);
+    unmap(H->own);
+    delete H;
+    return OSGPU_OK;
+}

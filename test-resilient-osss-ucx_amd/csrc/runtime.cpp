@@ -343,6 +343,16 @@ void *host_stage(const char *where, int me, size_t bytes)
 
 MemKind mem_kind(const void *p, int *dev)
 {
+    // virtual-memory heaps (heap.cpp) are device memory whatever the pointer
+    // query says about a hipMemMap'ed range
+    int hd = -1;
+    if (heap_created_range(p, 1, &hd)) {
+        if (dev) {
+            if (hd < 0 && hipGetDevice(&hd) != hipSuccess) hd = 0;
+            *dev = hd;
+        }
+        return MEM_DEVICE;
+    }
     hipPointerAttribute_t a;
     memset(&a, 0, sizeof(a));
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {

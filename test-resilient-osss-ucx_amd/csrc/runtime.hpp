@@ -75,6 +75,9 @@ struct HeapEntry {
 bool heap_segment(int pe, int seg, HeapEntry *out);
 bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off);
 bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out);
+// [p, p + n) inside a heap made by osgpu_heap_create (heap.cpp) -- the PE's
+// own range (*dev = its device) or a member's mapped here (*dev = -1)
+bool heap_created_range(const void *p, size_t n, int *dev);
 
 // ---------------------------------------------------------------- RCCL
 

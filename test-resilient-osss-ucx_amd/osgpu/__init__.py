@@ -112,6 +112,8 @@ def load() -> ctypes.CDLL:
     L.osgpu_heap_register_segment.argtypes = [i, i, vp, sz]
     L.osgpu_heap_unregister.argtypes = [i]
     L.osgpu_heap_translate.argtypes = [vp, i, i]
+    L.osgpu_heap_create.argtypes = [sz, i, i, i, vp, ctypes.POINTER(vp)]
+    L.osgpu_heap_destroy.argtypes = [vp]
     L.osgpu_heap_translate.restype = vp
     L.osgpu_ipc_get_handle.argtypes = [vp, vp]
     L.osgpu_ipc_open.argtypes = [vp]

@@ -91,6 +91,104 @@ def run_colls(L, rank, world, src_addr, tgt_addr, psync, out, tag, write, read):
         dist.barrier()
 
 
+def vmm_heap_mode(L, PES, rank, world):
+    """osgpu_heap_create: one contiguous device heap per PE (virtual-memory
+    chunks exported as dmabuf descriptors), every member's mapped here.
+    A symmetric double array of MP_VMM_BYTES (default 2.5 GiB) per PE --
+    beyond what one HIP IPC export can carry -- reduced on the team path
+    (owner-computes, host barriers) and on the pull path; the two 2.5 GiB
+    targets must be identical bit for bit (osgpu_compare, full size), a
+    sample must match the oracle's per-PE fold, and a long xor over the same
+    arrays must satisfy checksum(target) == xor of checksum(source_p) at
+    full size.  Then a small call (fused one-launch path) on the same heap."""
+    import numpy as np
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    nbytes = int(os.environ.get("MP_VMM_BYTES", str(5 << 29)))
+    n = nbytes // 8
+    nbytes = n * 8
+    al = 2 << 20
+    slot = (nbytes + al - 1) // al * al
+    off_t, off_p, off_s = slot, 2 * slot, 3 * slot      # team target, pull target, small
+    heap_bytes = 3 * slot + (16 << 20)
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    base_p = ctypes.c_void_p()
+    rc = L.osgpu_heap_create(heap_bytes, 0, 0, world, psync, ctypes.byref(base_p))
+    assert rc == 0, (rc, L.osgpu_last_error().decode())
+    assert not any(ctypes.string_at(psync, 512)), "pSync not reset"
+    base = base_p.value
+    res = {"heap_bytes": heap_bytes, "nbytes": nbytes}
+    # every member's heap is reachable at base + offset on every PE
+    for pe in range(world):
+        peer = L.osgpu_heap_translate(base + off_t, rank, pe)
+        assert peer, f"PE {pe}'s heap not registered"
+    wrk = (ctypes.c_byte * 4096)()
+    g = torch.Generator(device="cuda:0").manual_seed(0x7A5 + rank)
+    stage = torch.empty(n, dtype=torch.float64, device="cuda:0")
+    # signed values spread over 2^-20..2^20: FP sums depend on the fold order
+    stage.uniform_(-1.0, 1.0, generator=g)
+    stage.mul_(torch.exp2(torch.randint(-20, 21, (n,), device="cuda:0", generator=g,
+                                        dtype=torch.int32).to(torch.float64)))
+    osgpu.copy([base], [stage.data_ptr()], [nbytes])
+    torch.cuda.synchronize()
+    sync = lambda: PES.pes_barrier(0, 0, world, None)  # noqa: E731
+    sync()
+    paths = {}
+    for name, path, off in (("team", osgpu.PATH_AUTO, off_t), ("pull", osgpu.PATH_PULL, off_p)):
+        L.osgpu_set_path(path)
+        sync()
+        L.shmem_double_sum_to_all(base + off, base, n, 0, 0, world, wrk, psync)
+        paths[name] = osgpu.last_path()
+        sync()
+    L.osgpu_set_path(osgpu.PATH_AUTO)
+    res["paths"] = paths
+    res["team_vs_pull_mismatch"], _ = osgpu.compare(base + off_t, base + off_p, nbytes)
+    res["hash_team"] = osgpu.checksum("double", osgpu.CK_HASH, base + off_t, n)
+    # sampled oracle parity: every rank's source at the sampled indices
+    idx = torch.randint(0, n, (1 << 15,), generator=torch.Generator().manual_seed(99))
+    osgpu.copy([stage.data_ptr()], [base + off_t], [nbytes])
+    torch.cuda.synchronize()
+    got = stage[idx.cuda()].cpu().numpy()
+    osgpu.copy([stage.data_ptr()], [base], [nbytes])
+    torch.cuda.synchronize()
+    mine = stage[idx.cuda()].cpu()
+    allv = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    want = O.fold_with(O.op_elementwise, "double", "sum", [a.numpy() for a in allv], rank, 0, 0,
+                       world)
+    res["sample_mismatch"] = int(np.count_nonzero(got.view(np.uint64) != want.view(np.uint64)))
+    res["sample_checked"] = int(idx.numel())
+    # full-size checksum of checksums: long xor on the team path
+    L.shmem_long_xor_to_all(base + off_t, base, n, 0, 0, world, wrk, psync)
+    paths["xor"] = osgpu.last_path()
+    sync()
+    cks = [None] * world
+    dist.all_gather_object(cks, osgpu.checksum("long", osgpu.CK_XOR, base, n))
+    want_x = 0
+    for v in cks:
+        want_x ^= v
+    res["xor_checksum_ok"] = osgpu.checksum("long", osgpu.CK_XOR, base + off_t, n) == want_x
+    # a small object on the same heap: the fused one-launch path
+    m = 1000
+    small = torch.arange(m, dtype=torch.int32, device="cuda:0") + rank
+    osgpu.copy([base + off_s], [small.data_ptr()], [m * 4])
+    torch.cuda.synchronize()
+    sync()
+    L.shmem_int_sum_to_all(base + off_s + 8192, base + off_s, m, 0, 0, world, wrk, psync)
+    paths["small"] = osgpu.last_path()
+    osgpu.copy([small.data_ptr()], [base + off_s + 8192], [m * 4])
+    torch.cuda.synchronize()
+    want_s = world * np.arange(m, dtype=np.int32) + world * (world - 1) // 2
+    res["small_ok"] = bool(np.array_equal(small.cpu().numpy(), want_s))
+    del stage
+    sync()
+    L.osgpu_finalize()
+    assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
+    return res
+
+
 def device_heap_modes(L, PES, mode, rank, world):
     import time
     import torch
@@ -465,7 +563,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout"):
+            "timeout", "vmm"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -520,6 +618,8 @@ def main():
         res["out"] = out
     if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
+    if mode == "vmm":
+        res.update(vmm_heap_mode(L, PES, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096
         buf = PES.pes_heap(rank)

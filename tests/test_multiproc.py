@@ -293,6 +293,35 @@ def test_fused_collectives_processes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_vmm_heap_large_objects_processes(tmp_path):
+    """osgpu_heap_create with three processes on cuda:0: each PE's device heap
+    is ONE contiguous virtual range of dmabuf-exported chunks, mapped whole
+    into every member, so a 2.5 GiB symmetric array per PE (more than one HIP
+    IPC export carries) is base + offset on every PE like the
+    reference's heap (src/shmemc/comms.c:89-105).  shmem_double_sum_to_all
+    runs on the exact team kernel: its full 2.5 GiB target equals the pull
+    path's bit for bit on every PE (GPU compare), a 32 Ki sample equals the
+    oracle's per-PE fold, long xor satisfies checksum-of-checksums at full
+    size, and a small call on the same heap takes the fused path."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 3
+    res = launch("vmm", world, tmp_path, timeout=300)
+    for r in range(world):
+        x = res[r]
+        assert x["nbytes"] >= 5 << 29
+        assert x["paths"] == {"team": "team", "pull": "pull", "xor": "team",
+                              "small": "fused_team"}, x["paths"]
+        assert x["team_vs_pull_mismatch"] == 0, (r, x)
+        assert x["sample_mismatch"] == 0 and x["sample_checked"] == 1 << 15, (r, x)
+        assert x["xor_checksum_ok"], r
+        assert x["small_ok"], r
+    # fold orders differ per PE (PE 0 == PE 1 by a + b == b + a; PE 2 differs)
+    assert res[0]["hash_team"] == res[1]["hash_team"] != res[2]["hash_team"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fatal", [0, 1])
 def test_device_barrier_timeout(tmp_path, monkeypatch, fatal):
     """A member that never enters a fused call: the others' device barrier

@@ -18,7 +18,8 @@ step() {  # step NAME SECONDS CMD...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS} ;;
+    vmm)   step vmm 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_multiproc.py -k vmm ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 20 --warmup 5 ;;
     tune)  step tune 300 ./tools/tune_combine ;;
