@@ -333,6 +333,8 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         }
         fds.push_back(fd);
     }
+    DBG("%s PE %d: %zu chunks of %zu B created and exported (ok=%d)", where, c.me,
+        H->own.len.size(), chunk, (int) ok);
     if (ok && !map_chunks(H->own, gran, dev, true)) {
         set_err("%s: mapping the heap failed", where);
         ok = false;
@@ -360,6 +362,8 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     mine->chunk = (long) chunk;
     mine->raw_ptr = (long) (uintptr_t) H->own.base;
     mine->device = dev;
+    DBG("%s PE %d: own heap mapped at %p, listening (ok=%d)", where, c.me, (void *) H->own.base,
+        (int) ok);
     barrier(c);
 
     // everyone's layout; how many members from other processes will connect
@@ -373,6 +377,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     int expected = 0;
     for (int i = 0; i < PE_size; i++)
         if (c.pe_at(i) != c.me && msg[i].pid != (long) getpid()) expected++;
+    DBG("%s PE %d: layouts read, %d members in other processes", where, c.me, expected);
     std::atomic<int> served{0};
     std::thread server;
     if (lfd >= 0 && expected > 0 && mine->bytes > 0) {
@@ -382,6 +387,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
                 if (poll(&p, 1, kSetupTimeoutMs) <= 0) return;
                 const int s = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
                 if (s < 0) return;
+                DBG("osgpu_heap_create: serving connection %d", k);
                 if (send_fds(s, fds)) {
                     char ack;
                     (void) read_all(s, &ack, 1);  // the importer has its copies
@@ -408,7 +414,10 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         socklen_t al;
         sock_name(msg[i].pid, msg[i].nonce, &a, &al);
         std::vector<int> pf;
-        bool got = s >= 0 && connect(s, (sockaddr *) &a, al) == 0 && recv_fds(s, pf);
+        bool got = s >= 0 && connect(s, (sockaddr *) &a, al) == 0;
+        DBG("%s PE %d: connected to PE %d: %d", where, c.me, pe, (int) got);
+        got = got && recv_fds(s, pf);
+        DBG("%s PE %d: %zu descriptors from PE %d", where, c.me, pf.size(), pe);
         Mapping m;
         m.pe = pe;
         m.bytes = (size_t) msg[i].bytes;
@@ -416,14 +425,17 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         got = got && pf.size() == m.len.size();
         for (size_t k = 0; got && k < pf.size(); k++) {
             hipMemGenericAllocationHandle_t h;
-            if (hipMemImportFromShareableHandle(&h, (void *) (uintptr_t) pf[k],
-                                                hipMemHandleTypePosixFileDescriptor) !=
+            // ROCm reads the descriptor through the pointer (CUDA takes the
+            // value itself): passing the fd as an address faults
+            int fd = pf[k];
+            if (hipMemImportFromShareableHandle(&h, &fd, hipMemHandleTypePosixFileDescriptor) !=
                 hipSuccess) {
                 set_err("%s: importing PE %d's heap chunk %zu failed", where, pe, k);
                 got = false;
                 break;
             }
             m.h.push_back(h);
+            DBG("%s PE %d: imported chunk %zu of PE %d", where, c.me, k, pe);
         }
         for (int fd : pf) close(fd);
         if (s >= 0) {
@@ -445,6 +457,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             break;
         }
         base[i] = m.base;
+        DBG("%s PE %d: PE %d's heap mapped at %p", where, c.me, pe, (void *) m.base);
         H->peers.push_back(m);
     }
     if (server.joinable()) server.join();
@@ -453,6 +466,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     for (int fd : fds) close(fd);
 
     // every member's verdict
+    DBG("%s PE %d: served %d of %d, ok=%d", where, c.me, served.load(), expected, (int) ok);
     mine->status = ok ? 1 : 2;
     barrier(c);
     bool all_ok = ok;

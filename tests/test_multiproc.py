@@ -32,25 +32,32 @@ def _free_port():
 
 
 def launch(mode, world, tmp_path, timeout=600):
+    """Run `world` worker processes; each one's output goes to a log file as
+    it is written (under $MP_LOG_DIR when set, e.g. gpurun_out/, so a stalled
+    rank shows where it stopped), and its tail is reported on failure."""
     port = _free_port()
+    logdir = os.environ.get("MP_LOG_DIR") or str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, WORKER, mode, str(tmp_path)], env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                      text=True))
-    outs = []
-    for p in procs:
-        try:
-            out, _ = p.communicate(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
-        outs.append(out)
-    for p, out in zip(procs, outs):
-        assert p.returncode == 0, out[-3000:]
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+        log = os.path.join(logdir, f"{mode}_w{world}_rank{r}.log")
+        f = open(log, "w")
+        procs.append((subprocess.Popen([sys.executable, WORKER, mode, str(tmp_path)], env=env,
+                                       stdout=f, stderr=subprocess.STDOUT), f, log))
+    try:
+        for p, f, _ in procs:
+            p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        for q, _, _ in procs:
+            q.kill()
+        raise
+    finally:
+        for _, f, _ in procs:
+            f.close()
+    for p, _, log in procs:
+        assert p.returncode == 0, open(log).read()[-3000:]
     return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
 
 

@@ -5,6 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export MP_LOG_DIR=gpurun_out/mp
 step() {  # step NAME SECONDS CMD...
     local name=$1 secs=$2; shift 2
     echo "== $name: $*" | tee -a gpurun_out/steps.log
@@ -19,6 +20,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS} ;;
+    vmmprobe) step vmmprobe 200 python -u tools/vmm_probe.py 2 ;;
     vmm)   step vmm 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_multiproc.py -k vmm ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 20 --warmup 5 ;;
