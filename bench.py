@@ -651,11 +651,38 @@ def bench_multi(args):
 
     threading.Thread(target=watchdog, daemon=True).start()
 
-    # symmetric device heap in two segments (source, target): HIP IPC cannot
-    # export one allocation of >= 2 GiB here, so no segment is made that big
+    # ---- the device symmetric heap: ONE contiguous virtual range per PE
+    # (osgpu_heap_create: dmabuf chunks mapped into every member), holding
+    # the source and target of the main line and config 4's 1 Gi-double
+    # arrays.  If it cannot be built on some rank, the old form: two HIP IPC
+    # segments per PE (< 2 GiB each), and config 4 on RCCL.
     seg_bytes = (n * 8 + (2 << 20) - 1) // (2 << 20) * (2 << 20)
-    hsrc = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
-    htgt = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
+    n4 = args.c4_nreduce
+    c4_bytes = (n4 * 8 + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+    with_c4 = not args.no_extra
+    heap_bytes = 2 * seg_bytes + (2 * c4_bytes if with_c4 else 0)
+    state["phase"] = "heap"
+    mapped = []
+    bases = {}
+    heap_base = None
+    vmm_err = None
+    try:
+        heap_base = osgpu.heap_create(heap_bytes, 0, 0, world, psync.value)
+    except Exception as e:  # collective: the same verdict on every rank
+        vmm_err = repr(e)[:300]
+    team_ok = heap_base is not None
+    if team_ok:
+        hsrc = osgpu.device_view(heap_base, seg_bytes)
+        htgt = osgpu.device_view(heap_base + seg_bytes, seg_bytes)
+        for pe in range(world):
+            for s_, off in ((0, 0), (1, seg_bytes)):
+                bases[(pe, s_)] = L.osgpu_heap_translate(heap_base + off, rank, pe)
+        res["config"]["heap"] = (f"osgpu_heap_create: {heap_bytes} B contiguous per PE "
+                                 f"(VMM chunks, dmabuf)")
+    else:
+        res["heap_error"] = vmm_err
+        hsrc = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
+        htgt = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
     src = hsrc[: n * 8].view(torch.float64)
     tgt = htgt[: n * 8].view(torch.float64)
     src.uniform_(1.0, 2.0, generator=torch.Generator(device=dev).manual_seed(1000 + rank))
@@ -664,34 +691,33 @@ def bench_multi(args):
     def step():
         fn(tgt.data_ptr(), src.data_ptr(), n, 0, 0, world, wrk, psync)
 
-    # ---- IPC exchange of both segments, agreed on by every rank
-    state["phase"] = "ipc"
-    mapped = []
-    bases = {}
-    ok = seg_bytes < (2 << 30)
-    handles = []
-    for seg in (hsrc, htgt):
-        h = (ctypes.c_char * 64)()
-        ok = ok and L.osgpu_ipc_get_handle(ctypes.c_void_p(seg.data_ptr()), h) == 0
-        handles.append(bytes(h))
-    allh = [None] * world
-    dist.all_gather_object(allh, handles)
-    team_ok = _agree(dist, world, ok)
-    if team_ok:
-        for pe in range(world):
-            for s, seg in enumerate((hsrc, htgt)):
-                if pe == rank:
-                    base = seg.data_ptr()
-                else:
-                    base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(allh[pe][s]))
-                    ok = ok and bool(base)
-                    if base:
-                        mapped.append(base)
-                if base:
-                    L.osgpu_heap_register_segment(pe, s, ctypes.c_void_p(base), seg_bytes)
-                    bases[(pe, s)] = base
+    if not team_ok:
+        state["phase"] = "ipc"
+        ok = seg_bytes < (2 << 30)
+        handles = []
+        for seg in (hsrc, htgt):
+            h = (ctypes.c_char * 64)()
+            ok = ok and L.osgpu_ipc_get_handle(ctypes.c_void_p(seg.data_ptr()), h) == 0
+            handles.append(bytes(h))
+        allh = [None] * world
+        dist.all_gather_object(allh, handles)
         team_ok = _agree(dist, world, ok)
-    _log(rank, f"ipc heaps ready: {team_ok}")
+        if team_ok:
+            for pe in range(world):
+                for s_, seg in enumerate((hsrc, htgt)):
+                    if pe == rank:
+                        base = seg.data_ptr()
+                    else:
+                        base = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(allh[pe][s_]))
+                        ok = ok and bool(base)
+                        if base:
+                            mapped.append(base)
+                    if base:
+                        L.osgpu_heap_register_segment(pe, s_, ctypes.c_void_p(base), seg_bytes)
+                        bases[(pe, s_)] = base
+            team_ok = _agree(dist, world, ok)
+        res["config"]["heap"] = "HIP IPC segments (osgpu_heap_create failed)"
+    _log(rank, f"device heaps ready: {team_ok}")
 
     # ---- primary: exact team kernel over the IPC-mapped heaps
     if team_ok:
@@ -816,30 +842,46 @@ def bench_multi(args):
             _log(rank, "rccl done")
         except Exception as e:  # reported, never hidden
             res["rccl"] = {"error": repr(e)[:300]}
-    if rccl_ok and not args.no_extra:
+    # ---- BASELINE config 4: double sum, nreduce = 1 Gi (8 GiB per PE) over
+    # every GPU.  Exact path: the team kernel over the VMM heaps (each GPU
+    # folds its shard of every PE's target in that PE's own order); beside
+    # it ncclAllReduce (forced: FP within tolerance, not the reference order).
+    if with_c4 and (heap_base is not None or rccl_ok):
         state["phase"] = "config4"
+        c4 = {"nreduce": n4, "bytes_per_array": n4 * 8}
         try:
-            n4 = args.c4_nreduce
-            s4 = torch.empty(n4, dtype=torch.float64, device=dev)
-            t4 = torch.empty(n4, dtype=torch.float64, device=dev)
+            if heap_base is not None:
+                s4 = osgpu.device_view(heap_base + 2 * seg_bytes, n4 * 8).view(torch.float64)
+                t4 = osgpu.device_view(heap_base + 2 * seg_bytes + c4_bytes,
+                                       n4 * 8).view(torch.float64)
+            else:
+                s4 = torch.empty(n4, dtype=torch.float64, device=dev)
+                t4 = torch.empty(n4, dtype=torch.float64, device=dev)
             s4.uniform_(1.0, 2.0, generator=torch.Generator(device=dev).manual_seed(4000 + rank))
             torch.cuda.synchronize()
 
             def step4():
                 fn(t4.data_ptr(), s4.data_ptr(), n4, 0, 0, world, wrk, psync)
 
-            tt = _timed(step4, 3, 1, dist, torch)
-            res["config4"] = {"nreduce": n4, "path": "rccl", "ms_per_call": tt / 3 * 1e3,
-                              "value_GiBs": 3 * (world + 1) * n4 * 8 / tt / GIB,
-                              "algbw_GiBs": 3 * n4 * 8 / tt / GIB,
-                              "busbw_GBs": 3 * 2 * (world - 1) / world * n4 * 8 / tt / 1e9,
-                              "parity_vs_reference_order":
-                                  _sample_parity(rank, world, s4, t4, n4, "sum", dist)}
+            for name, path, usable in (("team", osgpu.PATH_AUTO, heap_base is not None),
+                                       ("rccl", osgpu.PATH_RCCL, rccl_ok)):
+                if not usable:
+                    continue
+                L.osgpu_set_path(path)
+                tt = _timed(step4, 3, 1, dist, torch)
+                c4[name] = {"path": osgpu.last_path(), "ms_per_call": tt / 3 * 1e3,
+                            "value_GiBs": 3 * (world + 1) * n4 * 8 / tt / GIB,
+                            "algbw_GiBs": 3 * n4 * 8 / tt / GIB,
+                            "xgmi_in_GBs_per_gpu": 3 * 2 * (world - 1) * (n4 * 8 // world) / tt / 1e9,
+                            "parity_vs_reference_order":
+                                _sample_parity(rank, world, s4, t4, n4, "sum", dist)}
+                _log(rank, f"config4 {name} done")
+            L.osgpu_set_path(osgpu.PATH_AUTO)
             del s4, t4
             torch.cuda.empty_cache()
-            _log(rank, "config4 done")
         except Exception as e:
-            res["config4"] = {"error": repr(e)[:300]}
+            c4["error"] = repr(e)[:300]
+        res["config4"] = c4
 
     # ---- BASELINE config 5: float min/max/prod, 128 Mi per PE, sources and
     # targets in pinned HOST memory: H2D + on-GPU exchange + D2H (STAGED path)
@@ -930,6 +972,10 @@ def bench_multi(args):
     for p in mapped:
         L.osgpu_ipc_close(ctypes.c_void_p(p))
     L.osgpu_finalize()
+    del hsrc, htgt, src, tgt
+    dist.barrier()
+    if heap_base is not None:
+        L.osgpu_heap_destroy(ctypes.c_void_p(heap_base))
     dist.barrier()
     dist.destroy_process_group()
 

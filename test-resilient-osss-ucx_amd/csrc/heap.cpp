@@ -66,6 +66,8 @@ struct Mapping {                     // one heap as mapped in this process
 
 struct Heap {                        // the heap a PE created, with its imports
     int pe = -1;
+    int seg = 0;                     // registry segment of every member's heap
+    std::vector<int> members;
     Mapping own;
     std::vector<Mapping> peers;      // members in other processes
 };
@@ -75,7 +77,7 @@ std::vector<Heap *> g_heaps;
 
 // what a PE publishes in pSync[16..] during osgpu_heap_create
 struct HeapMsg {
-    long pid, nonce, bytes, chunk, raw_ptr, status, device, pad;
+    long pid, nonce, bytes, chunk, raw_ptr, status, device, seg;
 };
 static_assert(sizeof(HeapMsg) <= (64 - kHeapPsync) * sizeof(long), "pSync room");
 
@@ -362,6 +364,10 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     mine->chunk = (long) chunk;
     mine->raw_ptr = (long) (uintptr_t) H->own.base;
     mine->device = dev;
+    for (int i = 0; i < PE_size; i++) H->members.push_back(c.pe_at(i));
+    // every heap of a member set gets its own registry segment: the lowest
+    // one free for every member here, agreed as the maximum over members
+    mine->seg = heap_free_segment(H->members);
     DBG("%s PE %d: own heap mapped at %p, listening (ok=%d)", where, c.me, (void *) H->own.base,
         (int) ok);
     barrier(c);
@@ -374,6 +380,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         else c.ops.getmem(&msg[i], mine, sizeof(HeapMsg), pe);
         if (msg[i].bytes <= 0) ok = false;
     }
+    for (int i = 0; i < PE_size; i++) H->seg = std::max(H->seg, (int) msg[i].seg);
     int expected = 0;
     for (int i = 0; i < PE_size; i++)
         if (c.pe_at(i) != c.me && msg[i].pid != (long) getpid()) expected++;
@@ -487,7 +494,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         return OSGPU_EPEER;
     }
     for (int i = 0; i < PE_size; i++)
-        osgpu_heap_register_segment(c.pe_at(i), 0, base[i], (size_t) msg[i].bytes);
+        osgpu_heap_register_segment(c.pe_at(i), H->seg, base[i], (size_t) msg[i].bytes);
     {
         std::lock_guard<std::mutex> lk(g_hmu);
         g_heaps.push_back(H);
@@ -516,8 +523,7 @@ extern "C" int osgpu_heap_destroy(void *base)
     }
     (void) hipDeviceSynchronize();
     // forget the registrations that point into these ranges
-    for (const Mapping &m : H->peers) osgpu_heap_unregister(m.pe);
-    osgpu_heap_unregister(H->pe);
+    for (int pe : H->members) heap_clear_segment(pe, H->seg);
     for (Mapping &m : H->peers) unmap(m);
     unmap(H->own);
     delete H;

@@ -242,6 +242,27 @@ bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out)
     return true;
 }
 
+// lowest segment index free on every PE of `pes` in this process's registry
+int heap_free_segment(const std::vector<int> &pes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (int seg = 0;; seg++) {
+        bool free = true;
+        for (int pe : pes)
+            if (pe >= 0 && (size_t) pe < g_heap.size() && (size_t) seg < g_heap[pe].size() &&
+                g_heap[pe][seg].base)
+                free = false;
+        if (free) return seg;
+    }
+}
+
+void heap_clear_segment(int pe, int seg)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (pe >= 0 && (size_t) pe < g_heap.size() && seg >= 0 && (size_t) seg < g_heap[pe].size())
+        g_heap[pe][seg] = HeapEntry();
+}
+
 // ---------------------------------------------------------------- RCCL
 
 Rccl g_rccl;

@@ -78,6 +78,9 @@ bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out);
 // [p, p + n) inside a heap made by osgpu_heap_create (heap.cpp) -- the PE's
 // own range (*dev = its device) or a member's mapped here (*dev = -1)
 bool heap_created_range(const void *p, size_t n, int *dev);
+// lowest segment index unused by every PE of `pes` (this process's registry)
+int heap_free_segment(const std::vector<int> &pes);
+void heap_clear_segment(int pe, int seg);
 
 // ---------------------------------------------------------------- RCCL
 

@@ -170,6 +170,32 @@ def compare(a: int, b: int, nbytes: int, stream: int | None = None):
     return bad.value, (None if first.value == (1 << 64) - 1 else first.value)
 
 
+def device_view(ptr: int, nbytes: int, dtype=None):
+    """A torch tensor aliasing `nbytes` of device memory at `ptr` -- e.g. a
+    heap made by osgpu_heap_create, whose virtual-memory range no torch
+    allocator owns -- through __cuda_array_interface__ (tests/bench only)."""
+    import torch
+
+    class _Mem:
+        def __init__(self):
+            self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1",
+                                             "data": (ptr, False), "version": 3,
+                                             "strides": None}
+
+    t = torch.as_tensor(_Mem(), device="cuda")
+    return t.view(dtype) if dtype is not None else t
+
+
+def heap_create(nbytes: int, PE_start: int, logPE_stride: int, PE_size: int, psync: int) -> int:
+    """osgpu_heap_create (collective): this PE's heap base; raises on failure."""
+    L = load()
+    base = ctypes.c_void_p()
+    rc = L.osgpu_heap_create(nbytes, PE_start, logPE_stride, PE_size, psync, ctypes.byref(base))
+    if rc != 0:
+        raise RuntimeError(f"osgpu_heap_create = {rc}: {L.osgpu_last_error().decode()}")
+    return base.value
+
+
 def last_path() -> str:
     """Name of the path the calling thread's last reduce-to-all call took."""
     return RAN[load().osgpu_last_path()]

@@ -51,6 +51,23 @@ def worker():
                 torch.cuda.synchronize()
                 ok = bool((buf == pe + 1).all())
                 log(f"read PE {pe} @+{off}: {'ok' if ok else 'WRONG'}")
+        # a torch view of the heap through __cuda_array_interface__
+        class _View:
+            def __init__(self, ptr, nb):
+                self.__cuda_array_interface__ = {"shape": (nb,), "typestr": "|u1",
+                                                 "data": (ptr, False), "version": 3,
+                                                 "strides": None}
+        try:
+            t = torch.as_tensor(_View(base.value, size), device="cuda:0")
+            t[: 1 << 20].fill_(7)
+            torch.cuda.synchronize()
+            osgpu.copy([buf.data_ptr()], [base.value], [1 << 20])
+            torch.cuda.synchronize()
+            log(f"torch view: device={t.device} ok={bool((buf == 7).all())} "
+                f"sum={int(t[:1 << 20].sum())}")
+            del t
+        except Exception as e:
+            log(f"torch view failed: {e!r}")
         dist.barrier()
         log(f"destroy rc={L.osgpu_heap_destroy(base)}")
         dist.barrier()
