@@ -726,7 +726,7 @@ def bench_multi(args):
         t = _timed(step, args.steps, args.warmup, dist, torch)
         res["value"] = args.steps * B / t / GIB
         res["ms_per_step"] = t / args.steps * 1e3
-        res["config"]["path"] = "p2p-team (exact owner-computes kernel over IPC-mapped HBM, xGMI)"
+        res["config"]["path"] = "p2p-team (exact owner-computes kernel over the members' mapped heaps, xGMI)"
         res["config"]["algbw_GiBs"] = n * 8 * args.steps / t / GIB
         # the exchange is link-bound: per step GPU g reads shard g of each
         # peer's source (n*8/P bytes per peer) and each peer h writes shard h

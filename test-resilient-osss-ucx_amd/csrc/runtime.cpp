@@ -1107,6 +1107,22 @@ int osgpu_combine(int type, int op, void *target, const void *const *srcs, int n
     return OSGPU_OK;
 }
 
+int osgpu_team_combine(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                       size_t nelems, void *hip_stream)
+{
+    if (!has_op(type, op) || P < 2 || P > osgpu::kMaxTeam || !dsts || !srcs) {
+        set_err("osgpu_team_combine: bad arguments");
+        return OSGPU_EINVAL;
+    }
+    hipStream_t st = hip_stream ? (hipStream_t) hip_stream : thread_stream("osgpu_team_combine");
+    hipError_t e = osgpu::launch_team(type, op, P, dsts, srcs, nelems, st);
+    if (e != hipSuccess) {
+        set_err("osgpu_team_combine: %s", hipGetErrorString(e));
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
 int osgpu_copy(void *const *dsts, const void *const *srcs, const size_t *bytes, int n,
                void *hip_stream)
 {

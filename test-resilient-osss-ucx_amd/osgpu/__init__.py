@@ -126,6 +126,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_get_stream.restype = vp
     L.osgpu_combine.argtypes = [i, i, vp, vp, i, sz, vp]
     L.osgpu_copy.argtypes = [vp, vp, vp, i, vp]
+    L.osgpu_team_combine.argtypes = [i, i, i, vp, vp, sz, vp]
     L.osgpu_has_op.argtypes = [i, i]
     L.osgpu_type_size.argtypes = [i]
     L.osgpu_type_size.restype = sz
