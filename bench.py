@@ -74,17 +74,20 @@ def parse():
 # N = 1
 # --------------------------------------------------------------------------
 
-def load_traffic():
-    """HBM bytes per launch of the combine kernel measured with rocprofv3
-    PMC counters (profiles/*traffic*.json, written by tools/pmc_traffic.py)."""
+def load_traffic(kernel="combine_vec_kernel<double, 0, 2>", n=None):
+    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters
+    (profiles/*traffic*.json, written by tools/pmc_traffic.py), newest round
+    last; None if no file covers that kernel at that nreduce."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
         try:
             with open(p) as f:
-                best = json.load(f)
+                d = json.load(f)
         except Exception:
-            pass
+            continue
+        if d.get("kernel") == kernel and (n is None or d.get("nreduce") == n):
+            best = d
     return best
 
 
@@ -230,6 +233,86 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
     return ts[len(ts) // 2], a, b, out
 
 
+def team_kernel_rate(L, torch, n, reps):
+    """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
+    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,2>
+    through the C ABI (osgpu_team_combine), one launch over all n elements --
+    the work the two PEs' shard launches of a 2-PE call do together: reads
+    both sources once, writes both targets (PE 0: x0+x1, PE 1: x1+x0).
+    Algorithmic bytes 4*n*8 per launch.  HIP events on the launch stream."""
+    dev = torch.device("cuda:0")
+    a = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0)
+    b = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0)
+    o0 = torch.empty(n, dtype=torch.float64, device=dev)
+    o1 = torch.empty(n, dtype=torch.float64, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
+    dsts = (ctypes.c_void_p * 2)(o0.data_ptr(), o1.data_ptr())
+    sp = ctypes.c_void_p(st.cuda_stream)
+    torch.cuda.synchronize()
+
+    def launch():
+        if L.osgpu_team_combine(5, 0, 2, dsts, srcs, n, sp) != 0:
+            raise RuntimeError(L.osgpu_last_error().decode())
+
+    for _ in range(3):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    torch.cuda.synchronize()
+    for e0, e1 in ev:
+        e0.record(st)
+        launch()
+        e1.record(st)
+    torch.cuda.synchronize()
+    ks = [e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev]
+    exact = bool(torch.equal(o0, a + b) and torch.equal(o1, b + a))
+    B = 4 * n * 8
+    kavg = sum(ks) / len(ks)
+    tr = load_traffic("team_vec_kernel<double, 0, 2, true>", n)
+    out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
+           "traffic": tr.get("bytes_per_launch") if tr else None,
+           "kernel": "osgpu::team_vec_kernel<double, SUM, 2, ordered>",
+           "kernel_avg_us": kavg * 1e6, "kernel_min_us": min(ks) * 1e6,
+           "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact": exact,
+           "note": "one launch over all nreduce elements = both PEs' shard launches of a 2-PE "
+                   "call; 2 reads + 2 writes of 8 B per element"}
+    del a, b, o0, o1
+    torch.cuda.empty_cache()
+    return out
+
+
+def stream_ceiling(L, torch, nbytes, reps=20):
+    """The copy kernel (csrc/copy.hip, one read + one write stream) over
+    nbytes: what a streaming kernel with writes moves on this box at this
+    footprint -- the practical ceiling the combine is compared with."""
+    dev = torch.device("cuda:0")
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
+    o = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    D = (ctypes.c_void_p * 1)(o.data_ptr())
+    S = (ctypes.c_void_p * 1)(a.data_ptr())
+    N = (ctypes.c_size_t * 1)(nbytes)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        assert L.osgpu_copy(D, S, N, 1, sp) == 0
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record(st)
+        L.osgpu_copy(D, S, N, 1, sp)
+        e1.record(st)
+    torch.cuda.synchronize()
+    ts = sorted(e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev)
+    med = ts[len(ts) // 2]
+    del a, o
+    torch.cuda.empty_cache()
+    return {"kernel": "copy_vec_kernel", "bytes_copied": nbytes, "us": med * 1e6,
+            "frac_of_8TBs": 2 * nbytes / med / 8e12}
+
+
 def extra_kernel_rates(L, torch):
     """The north-star statement (double sum at nreduce = 128 Mi: >= 80 % of
     HBM READ bandwidth) and BASELINE config 3 (long and/or/xor, 256 MiB per
@@ -238,11 +321,16 @@ def extra_kernel_rates(L, torch):
     n = 128 << 20
     t, a, b, o = kernel_rate(L, torch, 5, 0, n, 8, torch.float64,
                              lambda x, k: x.uniform_(1.0, 2.0))
-    out["north_star_double_sum_128Mi"] = {
-        "kernel_us": t * 1e6, "read_GBs": 2 * n * 8 / t / 1e9,
-        "read_frac_of_8TBs": 2 * n * 8 / t / 8e12, "frac_all_bytes": 3 * n * 8 / t / 8e12}
+    ns = {"kernel_us": t * 1e6, "read_GBs": 2 * n * 8 / t / 1e9,
+          "read_frac_of_8TBs": 2 * n * 8 / t / 8e12, "frac_all_bytes": 3 * n * 8 / t / 8e12}
     del a, b, o
     torch.cuda.empty_cache()
+    # the same footprint through the copy kernel (1 read + 1 write stream of
+    # 1.5 GiB each = the combine's 3 GiB): the box's streaming ceiling
+    ceil = stream_ceiling(L, torch, 3 * n * 8 // 2)
+    ns["copy_ceiling_same_bytes"] = ceil
+    ns["frac_of_copy_ceiling"] = ns["frac_all_bytes"] / ceil["frac_of_8TBs"]
+    out["north_star_double_sum_128Mi"] = ns
     n = 32 << 20
     c3 = {"nreduce": n, "bytes_per_array": n * 8}
     for name, code, ref in (("and", 2, lambda x, y: x & y), ("or", 3, lambda x, y: x | y),
@@ -352,19 +440,32 @@ def bench_single(args):
             res.update(extra_kernel_rates(L, torch))
         except Exception as e:  # report, never hide
             res["extra_kernels"] = {"error": repr(e)}
-    tr = load_traffic()
+    tr = load_traffic(n=n)
     res["roofline"] = {
         "bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
-        "traffic": tr.get("bytes_per_launch") if tr and tr.get("nreduce") == n else None,
+        "traffic": tr.get("bytes_per_launch") if tr else None,
         "kernel": "osgpu::combine_vec_kernel<double, SUM, 2>",
         "kernel_avg_us": kavg * 1e6,
         "kernel_min_us": min(kms) * 1e3,
         "algorithmic_bytes_per_launch": B,
     }
+    # the kernel the API dispatches (TEAM path), under the same roofline
+    try:
+        res["roofline_team"] = team_kernel_rate(L, torch, n, args.steps)
+    except Exception as e:  # report, never hide
+        res["roofline_team"] = {"error": repr(e)}
     if not args.no_api:
         try:
             res["api"] = api_call_time(n)
+            tcall = res["api"]["team"]["ms_per_call"] * 1e-3
+            res["roofline_call"] = {
+                "bound": "hbm", "achieved": 4 * n * 8 / tcall / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": 4 * n * 8 / tcall / 1e9 / HBM_PEAK_GBS,
+                "traffic": None, "ms_per_call": tcall * 1e3,
+                "what": "the whole shmem_double_sum_to_all call, 2 PEs (pthreads) on one GPU, "
+                        "default (TEAM) path: entry sync, 2 barriers, both PEs' shard launches, "
+                        "completion waits; 4*n*8 HBM bytes per call"}
         except Exception as e:  # report, never hide
             res["api"] = {"error": repr(e)}
         try:

@@ -79,15 +79,8 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
     const size_t t0 = (size_t) blockIdx.x * (kTeamBlock * U) + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const size_t j = t0 + (size_t) u * kTeamBlock;
-        if (j >= nvec) break;
-        TVec<T> in[P];
-#pragma unroll
-        for (int p = 0; p < P; p++)
-            in[p].v = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4 *>(a.src[p] + head) + j);
+    // fold one vector of every input into one vector of every output
+    auto fold_store = [&](TVec<T> (&in)[P], size_t j) {
         TVec<T> out[P];
 #pragma unroll
         for (int w = 0; w < W; w++) {
@@ -101,6 +94,38 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
 #pragma unroll
         for (int p = 0; p < P; p++)
             __builtin_nontemporal_store(out[p].v, reinterpret_cast<u32x4 *>(a.dst[p] + head) + j);
+    };
+    if (t0 + (size_t) (U - 1) * kTeamBlock < nvec) {
+        // whole tile: the loads of G vectors of every input are in flight
+        // before the first fold, as in combine_vec_kernel -- P*G*16 B per
+        // lane, not P*16 B per round trip.  G = U up to 4 inputs; above, two
+        // rounds of U/2 (all U*P at once spills the 8-input complex sum)
+        constexpr int G = P <= 4 ? U : (U > 1 ? U / 2 : 1);
+#pragma unroll
+        for (int g = 0; g < U; g += G) {
+            TVec<T> in[G][P];
+#pragma unroll
+            for (int u = 0; u < G; u++)
+#pragma unroll
+                for (int p = 0; p < P; p++)
+                    in[u][p].v = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4 *>(a.src[p] + head) + t0 +
+                        (size_t) (g + u) * kTeamBlock);
+#pragma unroll
+            for (int u = 0; u < G; u++) fold_store(in[u], t0 + (size_t) (g + u) * kTeamBlock);
+        }
+        return;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t j = t0 + (size_t) u * kTeamBlock;
+        if (j >= nvec) break;
+        TVec<T> in[P];
+#pragma unroll
+        for (int p = 0; p < P; p++)
+            in[p].v = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4 *>(a.src[p] + head) + j);
+        fold_store(in, j);
     }
 }
 

@@ -10,7 +10,11 @@ Corrections (MI355X_MICROARCH.md, section HBM / rocprofv3 PMC):
 The two counters come from separate passes (FETCH_SIZE needs 3 TCC slots,
 WRITE_SIZE 2; they do not fit one pass).
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR NREDUCE OUT.json
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR NREDUCE OUT.json [KERNEL [BYTES_PER_ELEM]]
+  KERNEL          substring of the kernel name (default the K=2 double-sum
+                  combine); BYTES_PER_ELEM algorithmic bytes per element per
+                  launch (default 24 = 2 reads + 1 write of 8 B; the team
+                  kernel at P = 2: 32)
 """
 import csv
 import glob
@@ -23,6 +27,7 @@ KERNEL = "combine_vec_kernel<double, 0, 2>"
 
 
 def values(d, counter):
+    global KERNEL
     vals = []
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(p) as f:
@@ -33,7 +38,11 @@ def values(d, counter):
 
 
 def main():
+    global KERNEL
     fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    if len(sys.argv) > 5:
+        KERNEL = sys.argv[5]
+    per_elem = int(sys.argv[6]) if len(sys.argv) > 6 else 24
     f = values(fdir, "FETCH_SIZE")
     w = values(wdir, "WRITE_SIZE")
     if not f or not w:
@@ -41,7 +50,7 @@ def main():
     fk, wk = statistics.median(f), statistics.median(w)
     read_b = 2.0 * fk * 1024.0
     write_b = wk * 1024.0
-    alg = 3 * n * 8
+    alg = per_elem * n
     res = {
         "kernel": KERNEL, "nreduce": n, "launches": [len(f), len(w)],
         "FETCH_SIZE_KiB_median": fk, "WRITE_SIZE_KiB_median": wk,
