@@ -61,6 +61,8 @@ constexpr int kFlagTicket = 16;   // last-workgroup tickets (u32): completion,
 constexpr int kFlagTicketIn = 17;  //   staged copy-in,
 constexpr int kFlagTicketOut = 18; //   staged copy-out
 constexpr int kFlagCount = 20;    // [20, 28): count[member] (collect: tag << 40 | source bytes)
+constexpr int kFlagGateIn = 28;   // entry gate: (epoch << 20 | attempt << 1 | go), my grid's
+constexpr int kFlagGateOut = 29;  //   verdict on the entry / exit wait (one decider per grid)
 constexpr int kCountBits = 40;
 constexpr int kFlagWords = 32;
 // fused grids: at most one workgroup of 256 lanes per CU of the GPU (256 on
@@ -72,9 +74,12 @@ struct FusedArgs {
     int q[kMaxTeam];                      // active-set index whose fold order dst[d] uses
     unsigned long long *flags[kMaxTeam];  // every member's flag area
     unsigned long long *mine;             // my flag area
-    int *err;                             // host-mapped: 1 arrive / 2 done timed out
+    int *err;                             // host-mapped: 1 arrive / 2 done not passed in time
     unsigned long long *done_host;        // host-mapped: epoch, written once the call is complete
-    unsigned long long epoch, timeout;    // timeout in wall-clock ticks
+    unsigned long long epoch, timeout;    // timeout: one wait slice, in wall-clock ticks
+    int resume;                           // 0 first launch, 1 continue at the entry barrier,
+                                          //   2 continue at the exit barrier
+    unsigned attempt;                     // launches of this call so far (gate keys)
     size_t n;                             // elements from src[p] / dst[d]
     size_t nvec, head, tail_start;        // filled by launch_fused
     int nedge, P, D, me;                  // me: my active-set index

@@ -37,8 +37,18 @@
 // their result slots, and after step 4 every workgroup waits for the done
 // flags and copies my result slot to my host target -- H2D, exchange and
 // D2H of the STAGED path in the same single launch.
-// Waits are bounded (wall clock); a timeout sets a host-mapped error word,
-// which the host turns into a fatal error, and the grid still drains.
+// Waits never hold the GPU for long, yet the barriers wait without bound,
+// like the reference's (src/shmemc/barrier.c:78-89 spinning in
+// shmemc_wait_eq_until64, src/shmemc/waituntil.c:57-71): ONE lane per grid
+// (the decider) waits at most one slice (FusedArgs::timeout) and publishes
+// the grid's verdict in a gate word of my flag area; every workgroup follows
+// the gate, so the whole grid either passes the barrier or ends before it
+// (no workgroup runs the body while another gave up).  On "not yet" the
+// decider sets the host-mapped error word (1 entry, 2 exit) and the host
+// launches a continuation (FusedArgs::resume) that picks up at that barrier
+// -- arrivals and done flags are epochs, so nothing is repeated or undone.
+// Only a member absent for longer than the device-barrier bound (none by
+// default) fails the call (runtime.cpp fused_complete).
 //
 // Co-residency: step 2 needs every member's workgroup 0 to run while my
 // workgroups wait.  Members on other GPUs always make progress; members
@@ -106,6 +116,42 @@ __device__ bool wait_epoch(const unsigned long long *f, int P, unsigned long lon
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     return true;
+}
+
+// Gate words (my flag area): the key names this call and this launch, so a
+// verdict of an earlier launch of the same call is never mistaken for this
+// one's; bit 0 = pass.
+__device__ __forceinline__ unsigned long long gate_key(const FusedArgs &a)
+{
+    return (a.epoch << 20) | ((unsigned long long) (a.attempt & 0x7ffffu) << 1);
+}
+
+__device__ __forceinline__ void gate_set(const FusedArgs &a, int word, bool pass)
+{
+    st_sys(a.mine + word, gate_key(a) | (pass ? 1ull : 0ull));
+}
+
+// one lane per workgroup: the grid's verdict (the decider always publishes
+// within one slice: it belongs to this grid and waits on nothing of it)
+__device__ __forceinline__ int gate_wait(const FusedArgs &a, int word)
+{
+    const unsigned long long key = gate_key(a);
+    unsigned long long v;
+    while (((v = ld_sys(a.mine + word)) & ~1ull) != key) __builtin_amdgcn_s_sleep(1);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return (int) (v & 1);
+}
+
+// Step 2: workgroup 0 waits for every member's arrival (one slice at most)
+// and decides for the grid.  False: not everyone is there yet (error word 1
+// set: the host continues the call with resume = 1).
+__device__ __forceinline__ bool entry_gate(const FusedArgs &a, int &s_go)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        gate_set(a, kFlagGateIn, wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1));
+    if (threadIdx.x == 0) s_go = gate_wait(a, kFlagGateIn);
+    __syncthreads();
+    return s_go;
 }
 
 // D outputs of one element: output d belongs to member q[d] and folds
@@ -194,22 +240,17 @@ __device__ void stage_copy(void *dst, const void *src, size_t nbytes)
     }
 }
 
-// Steps 1-2 (device form): workgroup 0 arrives in every member's area,
-// every workgroup waits for all arrivals.  False: timed out (error set).
-__device__ __forceinline__ bool fused_arrive(const FusedArgs &a, int &s_go)
-{
-    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
-        st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
-    if (threadIdx.x == 0)
-        s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
-    __syncthreads();
-    return s_go;
-}
-
 // Step 4 (device form): release, ticket; the last workgroup signals done,
-// waits for every member's done and publishes the host completion word.
-__device__ __forceinline__ void fused_done(const FusedArgs &a, int &s_go)
+// waits for every member's done (one slice) and publishes the host
+// completion word.  resume 2: only that wait, by workgroup 0.
+__device__ __forceinline__ void fused_done(const FusedArgs &a)
 {
+    if (a.resume == 2) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 &&
+            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
+            __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0 && last_workgroup(a, kFlagTicket)) {
@@ -217,7 +258,6 @@ __device__ __forceinline__ void fused_done(const FusedArgs &a, int &s_go)
         if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
             __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    (void) s_go;
 }
 
 // Grid-stride copy of one piece at the widest width both ends allow.
@@ -256,25 +296,24 @@ __device__ __forceinline__ void copy_piece(char *dst, const char *src, size_t nb
 __global__ __launch_bounds__(kFBlock) void fused_copy_kernel(FusedArgs a)
 {
     __shared__ int s_go;
-    if (a.host_in) {
-        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
-            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
-        if (threadIdx.x == 0)
-            s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
-        __syncthreads();
-        if (!s_go) return;
-    } else if (!fused_arrive(a, s_go)) {
-        return;
+    if (a.resume < 2) {
+        if (a.resume == 0 && a.host_in) {
+            stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
+                for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
+        } else if (a.resume == 0 && blockIdx.x == 0 && (int) threadIdx.x < a.P) {
+            st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
+        }
+        if (!entry_gate(a, s_go)) return;
+        const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
+        const size_t stride = (size_t) gridDim.x * kFBlock;
+        for (int d = 0; d < a.nseg; d++)
+            copy_piece(static_cast<char *>(a.dst[d]), static_cast<const char *>(a.src[d]),
+                       a.seg_bytes[d], tid, stride);
     }
-    const size_t tid = (size_t) blockIdx.x * kFBlock + threadIdx.x;
-    const size_t stride = (size_t) gridDim.x * kFBlock;
-    for (int d = 0; d < a.nseg; d++)
-        copy_piece(static_cast<char *>(a.dst[d]), static_cast<const char *>(a.src[d]),
-                   a.seg_bytes[d], tid, stride);
-    fused_done(a, s_go);
+    fused_done(a);
 }
 
 // collect (shmem_collect.cpp, src/shmemc/collect.c:24-69): contributions
@@ -297,28 +336,42 @@ __global__ __launch_bounds__(kFBlock) void fused_collect_kernel(FusedArgs a)
     __shared__ unsigned long long s_cnt[kMaxTeam];
     constexpr unsigned long long kCountMask = (1ull << kCountBits) - 1;
     const unsigned long long tag = a.count_tag & ((1ull << (64 - kCountBits)) - 1);
-    if (threadIdx.x == 0) s_go = 1;
-    if (blockIdx.x == 0 && (int) threadIdx.x < a.P)
+    if (a.resume == 2) {
+        fused_done(a);
+        return;
+    }
+    if (a.resume == 0 && blockIdx.x == 0 && (int) threadIdx.x < a.P)
         st_sys(a.flags[threadIdx.x] + kFlagCount + a.me,
                tag << kCountBits | ((unsigned long long) a.my_count & kCountMask));
-    __syncthreads();
-    if ((int) threadIdx.x < a.P) {
-        const unsigned long long *w = a.mine + kFlagCount + threadIdx.x;
-        const unsigned long long t0 = (unsigned long long) wall_clock64();
-        unsigned long long v;
-        while (((v = ld_sys(w)) >> kCountBits) != tag) {
-            if ((unsigned long long) wall_clock64() - t0 > a.timeout) {
-                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s_go = 0;
-                break;
+    // workgroup 0 decides for the grid: lanes i < P wait (one slice at most)
+    // for slot i to carry this call's tag
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) s_go = 1;
+        __syncthreads();
+        if ((int) threadIdx.x < a.P) {
+            const unsigned long long *w = a.mine + kFlagCount + threadIdx.x;
+            const unsigned long long t0 = (unsigned long long) wall_clock64();
+            while ((ld_sys(w) >> kCountBits) != tag) {
+                if ((unsigned long long) wall_clock64() - t0 > a.timeout) {
+                    s_go = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_s_sleep(1);
         }
-        s_cnt[threadIdx.x] = v & kCountMask;
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (!s_go) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            gate_set(a, kFlagGateIn, s_go);
+        }
     }
+    if (threadIdx.x == 0) s_go = gate_wait(a, kFlagGateIn);
     __syncthreads();
     if (!s_go) return;
+    // the slots hold this call's counts until every member has passed its
+    // done barrier
+    if ((int) threadIdx.x < a.P) s_cnt[threadIdx.x] = ld_sys(a.mine + kFlagCount + threadIdx.x) & kCountMask;
+    __syncthreads();
     unsigned long long total = 0;
     bool fits = true;
     for (int i = 0; i < a.P; i++) {
@@ -342,100 +395,117 @@ __global__ __launch_bounds__(kFBlock) void fused_collect_kernel(FusedArgs a)
             off += s_cnt[i];
         }
     }
-    fused_done(a, s_go);
+    fused_done(a);
 }
 
 template <typename T, int OP, bool VEC>
 __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
 {
     __shared__ int s_go;
-    const bool tr = a.trace && blockIdx.x == 0 && threadIdx.x == 0;
+    const bool tr = a.trace && blockIdx.x == 0 && threadIdx.x == 0 && a.resume == 0;
     if (tr) a.trace[0] = (unsigned long long) wall_clock64();
-    // 1. arrive (src/reductions.c:82 -- my source is ready, my target free).
-    // Staged form: my host source is first copied into my staging slot by
-    // the whole grid; the last workgroup to finish its part arrives.
-    if (a.host_in) {
-        stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+    if (a.resume < 2) {
+        // 1. arrive (src/reductions.c:82 -- my source is ready, my target
+        // free).  Staged form: my host source is first copied into my staging
+        // slot by the whole grid; the last workgroup to finish its part
+        // arrives.  A continuation (resume 1) has arrived already.
+        if (a.resume == 0 && a.host_in) {
+            stage_copy(a.stage_mine, a.host_in, a.host_bytes);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
+                for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
+        } else if (a.resume == 0 && blockIdx.x == 0 && (int) threadIdx.x < a.P) {
+            st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
+        }
+        // 2. every member's arrival (one decider, the grid follows)
+        if (!entry_gate(a, s_go)) return;
+        if (tr) a.trace[1] = (unsigned long long) wall_clock64();
+
+        // 3. combine body
+        if (VEC) {
+            constexpr int W = 16 / sizeof(T);
+            if (blockIdx.x == 0 && (int) threadIdx.x < a.nedge) {
+                const size_t e =
+                    threadIdx.x < a.head ? threadIdx.x : a.tail_start + (threadIdx.x - a.head);
+                do_elem<T, OP>(a, e);
+            }
+            const size_t stride = (size_t) gridDim.x * kFBlock;
+            for (size_t j = (size_t) blockIdx.x * kFBlock + threadIdx.x; j < a.nvec; j += stride) {
+                FVec<T> in[kMaxTeam];
+#pragma unroll
+                for (int p = 0; p < kMaxTeam; p++)
+                    if (p < a.P)
+                        in[p].v = __builtin_nontemporal_load(
+                            reinterpret_cast<const u32x4 *>(static_cast<const T *>(a.src[p]) +
+                                                            a.head) + j);
+                FVec<T> out[kMaxTeam];
+#pragma unroll
+                for (int w = 0; w < W; w++) {
+                    T x[kMaxTeam], r[kMaxTeam];
+#pragma unroll
+                    for (int p = 0; p < kMaxTeam; p++) x[p] = p < a.P ? in[p].e[w] : T();
+                    fold_outputs<T, OP>(x, a.P, a.D, a.q, r);
+#pragma unroll
+                    for (int d = 0; d < kMaxTeam; d++) out[d].e[w] = r[d];
+                }
+#pragma unroll
+                for (int d = 0; d < kMaxTeam; d++)
+                    if (d < a.D)
+                        store_out(
+                            reinterpret_cast<u32x4 *>(static_cast<T *>(a.dst[d]) + a.head) + j,
+                            out[d].v);
+            }
+        } else {
+            const size_t stride = (size_t) gridDim.x * kFBlock;
+            for (size_t i = (size_t) blockIdx.x * kFBlock + threadIdx.x; i < a.n; i += stride)
+                do_elem<T, OP>(a, i);
+        }
+
+        // 4. completion (src/reductions.c:113): my stores and reads are
+        // done.  Every wave waits for its own stores, then ONE lane per
+        // workgroup makes them visible system-wide (an L2 writeback per fence:
+        // one per workgroup, not one per wave) and takes a ticket; the last
+        // workgroup signals done and waits for every member's (one slice).
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
-        if (threadIdx.x == 0 && last_workgroup(a, kFlagTicketIn))
-            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagArrive + a.me, a.epoch);
-    } else if (blockIdx.x == 0 && (int) threadIdx.x < a.P) {
-        st_sys(a.flags[threadIdx.x] + kFlagArrive + a.me, a.epoch);
-    }
-    // 2. wait for every member's arrival
-    if (threadIdx.x == 0)
-        s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
-    __syncthreads();
-    if (!s_go) return;
-    if (tr) a.trace[1] = (unsigned long long) wall_clock64();
-
-    // 3. combine body
-    if (VEC) {
-        constexpr int W = 16 / sizeof(T);
-        if (blockIdx.x == 0 && (int) threadIdx.x < a.nedge) {
-            const size_t e =
-                threadIdx.x < a.head ? threadIdx.x : a.tail_start + (threadIdx.x - a.head);
-            do_elem<T, OP>(a, e);
-        }
-        const size_t stride = (size_t) gridDim.x * kFBlock;
-        for (size_t j = (size_t) blockIdx.x * kFBlock + threadIdx.x; j < a.nvec; j += stride) {
-            FVec<T> in[kMaxTeam];
-#pragma unroll
-            for (int p = 0; p < kMaxTeam; p++)
-                if (p < a.P)
-                    in[p].v = __builtin_nontemporal_load(
-                        reinterpret_cast<const u32x4 *>(static_cast<const T *>(a.src[p]) +
-                                                        a.head) + j);
-            FVec<T> out[kMaxTeam];
-#pragma unroll
-            for (int w = 0; w < W; w++) {
-                T x[kMaxTeam], r[kMaxTeam];
-#pragma unroll
-                for (int p = 0; p < kMaxTeam; p++) x[p] = p < a.P ? in[p].e[w] : T();
-                fold_outputs<T, OP>(x, a.P, a.D, a.q, r);
-#pragma unroll
-                for (int d = 0; d < kMaxTeam; d++) out[d].e[w] = r[d];
-            }
-#pragma unroll
-            for (int d = 0; d < kMaxTeam; d++)
-                if (d < a.D)
-                    store_out(reinterpret_cast<u32x4 *>(static_cast<T *>(a.dst[d]) + a.head) + j,
-                              out[d].v);
-        }
-    } else {
-        const size_t stride = (size_t) gridDim.x * kFBlock;
-        for (size_t i = (size_t) blockIdx.x * kFBlock + threadIdx.x; i < a.n; i += stride)
-            do_elem<T, OP>(a, i);
-    }
-
-    // 4. completion (src/reductions.c:113): my stores and reads are done.
-    // Every wave waits for its own stores, then ONE lane per workgroup makes
-    // them visible system-wide (an L2 writeback per fence: one per workgroup,
-    // not one per wave) and takes a ticket; the last workgroup signals.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    if (tr) a.trace[2] = (unsigned long long) wall_clock64();
-    if (threadIdx.x == 0) {
-        s_go = last_workgroup(a, kFlagTicket);
-        if (tr) a.trace[3] = (unsigned long long) wall_clock64();
-        if (s_go) {
-            if (a.trace) a.trace[4] = a.trace[5] = (unsigned long long) wall_clock64();
-            for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
-            if (!a.host_out && wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2)) {
-                if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
-                // the host returns on this word, without waiting for the launch to retire
-                __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tr) a.trace[2] = (unsigned long long) wall_clock64();
+        if (threadIdx.x == 0) {
+            const bool last = last_workgroup(a, kFlagTicket);
+            if (tr) a.trace[3] = (unsigned long long) wall_clock64();
+            if (last) {
+                if (a.trace) a.trace[4] = a.trace[5] = (unsigned long long) wall_clock64();
+                for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
+                const bool all = wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2);
+                if (!a.host_out) {
+                    if (all) {
+                        if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
+                        // the host returns on this word, without waiting for
+                        // the launch to retire
+                        __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                } else {
+                    gate_set(a, kFlagGateOut, all);
+                }
             }
         }
+        if (!a.host_out) return;
+    } else if (!a.host_out) {
+        // continuation at the exit barrier, device form: the done wait only
+        if (blockIdx.x == 0 && threadIdx.x == 0 &&
+            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
+            __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // continuation at the exit barrier, staged form: workgroup 0 decides
+        gate_set(a, kFlagGateOut,
+                 wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2));
     }
-    if (!a.host_out) return;
     // Staged form: once every member has written its shard of my result
-    // slot, the whole grid copies it to my host target; the last workgroup
-    // to finish publishes the completion word.
-    if (threadIdx.x == 0)
-        s_go = wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2);
+    // slot (the exit gate passed), the whole grid copies it to my host
+    // target; the last workgroup to finish publishes the completion word.
+    if (threadIdx.x == 0) s_go = gate_wait(a, kFlagGateOut);
     __syncthreads();
     if (!s_go) return;
     stage_copy(a.host_out, a.stage_result, a.host_bytes);

@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -705,30 +706,33 @@ size_t fused_max_bytes()
 
 std::map<std::tuple<int, int, int, int, int>, SyncSet> g_sync;  // (me, set, device)
 
-// Completion of a fused call: spin on the host-mapped word the kernel's
+// Completion of a fused launch: spin on the host-mapped word the kernel's
 // last workgroup writes once every member is done (no wait for the launch to
-// retire); the stream is polled now and then so a launch that ended without
-// writing it (a timed-out barrier) is noticed.
-void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned long long epoch)
+// retire); also return when the launch reports a barrier it did not pass in
+// its slice (error word), or when the stream ends without either.
+static void fused_wait(const char *where, const SyncSet &S, hipStream_t st,
+                       unsigned long long epoch)
 {
     for (unsigned it = 1;; it++) {
         if (__atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= epoch) return;
-        if (__atomic_load_n(S.err_h, __ATOMIC_RELAXED)) return;  // fused_check reports it
+        if (__atomic_load_n(S.err_h, __ATOMIC_ACQUIRE)) return;
         if ((it & 4095) == 0) {
             const hipError_t q = hipStreamQuery(st);
-            if (q == hipSuccess) return;  // ended; fused_check tells done from failed
+            if (q == hipSuccess) return;  // ended; the caller tells done from failed
             if (q != hipErrorNotReady) fatal(where, "fused launch: %s", hipGetErrorString(q));
         }
         __builtin_ia32_pause();
     }
 }
 
-// Device-barrier policy (osgpu_set_device_barrier): wait bound and whether
-// a timed-out call aborts the process (default) or is reported.
-double g_dbar_secs = -1;  // <= 0: OSGPU_DEVICE_BARRIER_TIMEOUT_S, else 10 s
+// Device-barrier policy (osgpu_set_device_barrier): how long a member may
+// stay away before the call fails (<= 0: OSGPU_DEVICE_BARRIER_TIMEOUT_S, else
+// without bound, the reference's barrier), and whether that failure aborts
+// the process (default) or is reported.
+double g_dbar_secs = -1;
 int g_dbar_fatal = 1;
 
-unsigned long long fused_timeout_ticks(const SyncSet &S)
+static double fused_bound_secs()
 {
     double secs;
     {
@@ -737,25 +741,42 @@ unsigned long long fused_timeout_ticks(const SyncSet &S)
     }
     if (secs <= 0) {
         const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
-        secs = e ? atof(e) : 10.0;
-        if (secs <= 0) secs = 10.0;
+        secs = e ? atof(e) : 0.0;
     }
-    return (unsigned long long) (secs * 1e3 * S.rate_khz);
+    return secs > 0 ? secs : 0.0;
 }
 
-bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool word)
+// One wait slice of a fused launch (OSGPU_DEVICE_BARRIER_SLICE_MS, default
+// 100 ms): the longest a launch holds its CUs waiting at a device barrier.
+static double fused_slice_secs()
 {
-    const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
-    const bool incomplete = word && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) < epoch;
-    if (!err && !incomplete) return true;
+    static const double s = [] {
+        const char *e = getenv("OSGPU_DEVICE_BARRIER_SLICE_MS");
+        const double ms = e ? atof(e) : 100.0;
+        return (ms > 0 ? ms : 100.0) * 1e-3;
+    }();
+    return s;
+}
+
+static double now_secs()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+static bool fused_fail(const char *where, SyncSet &S, int err, unsigned long long epoch,
+                       double absent)
+{
     char msg[256];
     if (err == 3)
         snprintf(msg, sizeof(msg),
                  "collect: a member's contribution exceeds its source object in the heap");
     else if (err)
         snprintf(msg, sizeof(msg),
-                 "device barrier (%s) timed out: a member of the active set did not enter or "
-                 "finish the call", err == 1 ? "entry" : "exit");
+                 "device barrier (%s): a member of the active set stayed away for %.2f s, "
+                 "longer than the device-barrier bound",
+                 err == 1 ? "entry" : "exit", absent);
     else
         snprintf(msg, sizeof(msg), "fused launch ended without completing epoch %llu", epoch);
     int fatal_policy;
@@ -770,6 +791,40 @@ bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool w
     __atomic_store_n(S.err_h, 0, __ATOMIC_RELEASE);
     S.ok = false;
     return false;
+}
+
+thread_local int t_continuations = 0;  // of the calling thread's last fused call
+
+bool fused_complete(const char *where, SyncSet &S, hipStream_t st, osgpu::FusedArgs &a,
+                    const std::function<hipError_t(const osgpu::FusedArgs &)> &launch)
+{
+    t_continuations = 0;
+    const double slice = fused_slice_secs();
+    a.timeout = (unsigned long long) (slice * 1e3 * S.rate_khz);
+    a.resume = 0;
+    a.attempt = 0;
+    hipError_t e = launch(a);
+    if (e != hipSuccess) fatal(where, "fused launch: %s", hipGetErrorString(e));
+    const double bound = fused_bound_secs();
+    double since = -1;  // when the current wait began (first unpassed barrier)
+    for (;;) {
+        fused_wait(where, S, st, a.epoch);
+        const int err = __atomic_load_n(S.err_h, __ATOMIC_ACQUIRE);
+        if (!err && __atomic_load_n(S.done_h, __ATOMIC_ACQUIRE) >= a.epoch) return true;
+        if (err != 1 && err != 2) return fused_fail(where, S, err, a.epoch, 0);
+        // a member has not reached the barrier yet: continue there
+        const double now = now_secs();
+        if (since < 0 || a.resume != err) since = now - slice;
+        if (bound > 0 && now - since > bound) return fused_fail(where, S, err, a.epoch, now - since);
+        __atomic_store_n(S.err_h, 0, __ATOMIC_RELEASE);
+        a.resume = err;
+        a.attempt++;
+        t_continuations++;
+        DBG("%s: epoch %llu: %s barrier not passed yet, continuation %u", where, a.epoch,
+            err == 1 ? "entry" : "exit", a.attempt);
+        e = launch(a);
+        if (e != hipSuccess) fatal(where, "fused continuation launch: %s", hipGetErrorString(e));
+    }
 }
 
 SyncSet *sync_setup(const Coll &c)
@@ -1256,6 +1311,8 @@ int osgpu_shard_range(long long nreduce, int PE_size, int idx, int elem_bytes, l
     *hi = (idx == PE_size - 1) ? nreduce : (start + cnt) * g;
     return OSGPU_OK;
 }
+
+int osgpu_last_continuations(void) { return t_continuations; }
 
 const char *osgpu_last_error(void) { return g_err; }
 

@@ -11,7 +11,10 @@
 #include <stdio.h>
 #include <unistd.h>
 
+#include <functional>
 #include <vector>
+
+#include "combine.hpp"
 
 namespace osgpu {
 namespace rt {
@@ -181,11 +184,16 @@ struct SyncSet {
     unsigned long long *cnt_h = nullptr, *cnt_d = nullptr;    // host-mapped collect counts
 };
 SyncSet *sync_setup(const Coll &c);
-// wait for a fused launch's completion word (epoch) / report a failed one
-void fused_wait(const char *where, const SyncSet &S, hipStream_t st, unsigned long long epoch);
-// false (not fatal by policy): the call failed, the set's fused path is off
-bool fused_check(const char *where, SyncSet &S, unsigned long long epoch, bool word);
-unsigned long long fused_timeout_ticks(const SyncSet &S);
+// Launch a fused call (`launch(a)` on stream st, a.epoch set) and drive it to
+// completion: whenever the launch ended at a device barrier that a member
+// had not reached within one wait slice, launch its continuation there
+// (a.resume) -- the barrier waits without bound, the GPU is never held for
+// more than a slice.  true: complete (the host completion word carries
+// a.epoch).  false (not fatal by policy): a member stayed away longer than
+// the device-barrier bound, or a collect contribution was out of bounds;
+// the call failed and the set's fused path is off.
+bool fused_complete(const char *where, SyncSet &S, hipStream_t st, osgpu::FusedArgs &a,
+                    const std::function<hipError_t(const osgpu::FusedArgs &)> &launch);
 
 // Team exchange form: 0 pull (remote reads, default), 1 push (remote writes
 // through the members' staging inboxes); osgpu_set_team_exchange /

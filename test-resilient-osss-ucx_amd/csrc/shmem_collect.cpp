@@ -229,23 +229,21 @@ void run_fused_copy(const CCall &c, SyncSet &S, const std::vector<osgpu::CopySeg
     a.err = S.err_d;
     a.done_host = S.done_d;
     a.epoch = ++S.epoch;
-    a.timeout = fused_timeout_ticks(S);
     a.P = c.PE_size;
     a.me = S.idx;
     a.max_blocks = S.max_blocks;
     DBG("%s PE %d: fused copy, %d pieces, epoch %llu", c.name, c.me, a.nseg, a.epoch);
     entry_order(c.name, st);
-    hipError_t e = osgpu::launch_fused_copy(a, st);
-    if (e != hipSuccess) fatal(c.name, "fused copy launch: %s", hipGetErrorString(e));
-    const bool scratch = out != (char *) c.target;
-    if (scratch) {  // every reader of my source is done when the launch ends
+    if (!fused_complete(c.name, S, st, a,
+                        [&](const osgpu::FusedArgs &x) { return osgpu::launch_fused_copy(x, st); })) {
+        t_last_coll = OSGPU_RAN_FUSED_FAILED;
+        return;
+    }
+    if (out != (char *) c.target) {  // every reader of my source is done: exit barrier passed
         if (c.out_bytes)
             HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.out_bytes, hipMemcpyDeviceToDevice, st));
         stream_wait(c.name, st);
-    } else {
-        fused_wait(c.name, S, st, a.epoch);
     }
-    if (!fused_check(c.name, S, a.epoch, !scratch)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
 }
 
 // Host heaps pinned on every PE (osgpu_host_register): a small broadcast /
@@ -286,17 +284,15 @@ bool run_fused_staged_copy(const CCall &c, StageSet &G)
     a.err = S->err_d;
     a.done_host = S->done_d;
     a.epoch = ++S->epoch;
-    a.timeout = fused_timeout_ticks(*S);
     a.P = c.PE_size;
     a.me = S->idx;
     a.max_blocks = S->max_blocks;
     DBG("%s PE %d: fused staged copy, %d pieces, epoch %llu", c.name, c.me, a.nseg, a.epoch);
     hipStream_t st = pe_stream(c.name, c.me);
     entry_order(c.name, st);
-    hipError_t e = osgpu::launch_fused_copy(a, st);
-    if (e != hipSuccess) fatal(c.name, "fused staged copy launch: %s", hipGetErrorString(e));
-    fused_wait(c.name, *S, st, a.epoch);
-    if (!fused_check(c.name, *S, a.epoch, true)) t_last_coll = OSGPU_RAN_FUSED_FAILED;
+    if (!fused_complete(c.name, *S, st, a,
+                        [&](const osgpu::FusedArgs &x) { return osgpu::launch_fused_copy(x, st); }))
+        t_last_coll = OSGPU_RAN_FUSED_FAILED;
     return true;
 }
 
@@ -344,7 +340,6 @@ int fused_collect(CCall &c)
     a.done_host = S->done_d;
     a.counts_host = S->cnt_d;
     a.epoch = ++S->epoch;
-    a.timeout = fused_timeout_ticks(*S);
     a.P = P;
     a.me = S->idx;
     a.max_blocks = S->max_blocks;
@@ -354,10 +349,9 @@ int fused_collect(CCall &c)
     a.copy_limit = lim;
     DBG("%s PE %d: fused collect, %zu bytes mine, epoch %llu", c.name, c.me, mine, a.epoch);
     entry_order(c.name, st);
-    hipError_t e = osgpu::launch_fused_collect(a, st);
-    if (e != hipSuccess) fatal(c.name, "fused collect launch: %s", hipGetErrorString(e));
-    fused_wait(c.name, *S, st, a.epoch);
-    if (!fused_check(c.name, *S, a.epoch, true)) {
+    if (!fused_complete(c.name, *S, st, a, [&](const osgpu::FusedArgs &x) {
+            return osgpu::launch_fused_collect(x, st);
+        })) {
         t_last_coll = OSGPU_RAN_FUSED_FAILED;
         return 2;
     }

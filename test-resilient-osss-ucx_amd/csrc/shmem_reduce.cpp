@@ -287,7 +287,6 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     a.err = S.err_d;
     a.done_host = S.done_d;
     a.epoch = ++S.epoch;
-    a.timeout = fused_timeout_ticks(S);
     a.n = (size_t) (hi - lo);
     a.P = P;
     a.me = idx;
@@ -313,13 +312,15 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
     }();
     a.trace = trace;
     entry_order(c.name, st);
-    hipError_t e = osgpu::launch_fused(c.type, c.op, a, st);
-    if (e != hipSuccess) fatal(c.name, "fused launch: %s", hipGetErrorString(e));
-    if (overlap) {
+    if (!fused_complete(c.name, S, st, a, [&](const osgpu::FusedArgs &x) {
+            return osgpu::launch_fused(c.type, c.op, x, st);
+        })) {
+        t_last_path = OSGPU_RAN_FUSED_FAILED;
+        return;
+    }
+    if (overlap) {  // every reader of my source is done: the call passed its exit barrier
         HIPCHK(c.name, hipMemcpyAsync(c.target, out, c.nbytes, hipMemcpyDeviceToDevice, st));
         stream_wait(c.name, st);
-    } else {
-        fused_wait(c.name, S, st, a.epoch);
     }
     if (trace) {
         const double tk = 1e3 / S.rate_khz;  // us per tick of the device wall clock
@@ -329,7 +330,6 @@ void run_fused(const Call &c, SyncSet &S, const std::vector<const void *> &srcs,
                 (trace[3] - trace[2]) * tk, (trace[4] - trace[3]) * tk,
                 (trace[6] - trace[5]) * tk);
     }
-    if (!fused_check(c.name, S, a.epoch, !overlap)) t_last_path = OSGPU_RAN_FUSED_FAILED;
 }
 
 // RCCL's arithmetic for a (type, op), or false.

@@ -312,6 +312,87 @@ def device_heap_modes(L, PES, mode, rank, world):
             res["error"] = L.osgpu_last_error().decode()
         dist.barrier()
         L.osgpu_set_device_barrier(-1, 1)
+    if mode == "late":
+        # The last member enters every call MP_LATE_S seconds after the
+        # others (entry barrier), on the team and pull forms of the fused
+        # reduce, a fused fcollect and a fused collect; then MP_JITTER_CALLS
+        # calls whose members enter with random delays of up to 2 ms.  With a
+        # short wait slice (OSGPU_DEVICE_BARRIER_SLICE_MS from the test)
+        # these go through many continuations at both barriers.  Every
+        # result must be bit-exact and nothing may abort: the device barrier
+        # waits without bound, like the reference's.
+        import random
+        late = float(os.environ.get("MP_LATE_S", "1.5"))
+        lat = {}
+        L.osgpu_last_continuations.restype = ctypes.c_int
+        n = 4099
+        for ci, (t, op, path) in enumerate((("int", "sum", osgpu.PATH_AUTO),
+                                            ("double", "sum", osgpu.PATH_AUTO),
+                                            ("float", "prod", osgpu.PATH_PULL),
+                                            ("complexd", "prod", osgpu.PATH_AUTO))):
+            s_ = np.dtype(O.NP_DTYPE[t]).itemsize
+            src = O.team_inputs(t, world, n, 0x1A7E + ci, "wide")
+            want = O.to_all(t, op, src)[rank]
+            toff = (n * s_ + 4095) // 4096 * 4096
+            L.osgpu_set_path(path)
+            put(0, src[rank])
+            heap[toff:toff + n * s_].fill_(0x5A)
+            torch.cuda.synchronize()
+            sync()
+            if rank == world - 1:
+                time.sleep(late)
+            t0 = time.perf_counter()
+            getattr(L, f"shmem_{t}_{op}_to_all")(dev0 + toff, dev0, n, 0, 0, world, wrk, psync)
+            dt = time.perf_counter() - t0
+            got = heap[toff:toff + n * s_].cpu().numpy()
+            lat[f"{t}/{op}/{path}"] = [bool(np.array_equal(got, want.view(np.uint8).reshape(-1))),
+                                       osgpu.last_path(), dt, L.osgpu_last_continuations()]
+            sync()
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        # fused fcollect64 and collect32 with the last member late
+        for kind, bits in (("fcollect", 64), ("collect", 32)):
+            cnt = 300 + 7 * rank if kind == "collect" else 300
+            esz = bits // 8
+            raw = np.arange(cnt * esz, dtype=np.uint8) + rank
+            counts = [300 + 7 * r if kind == "collect" else 300 for r in range(world)]
+            want = np.concatenate([np.arange(c * esz, dtype=np.uint8) + r
+                                   for r, c in enumerate(counts)])
+            coff = 1 << 20
+            put(0, raw)
+            heap[coff:coff + want.size].fill_(0x5A)
+            torch.cuda.synchronize()
+            sync()
+            if rank == world - 1:
+                time.sleep(late)
+            t0 = time.perf_counter()
+            osgpu.coll(kind, bits)(dev0 + coff, dev0, cnt, 0, 0, world, psync)
+            dt = time.perf_counter() - t0
+            got = heap[coff:coff + want.size].cpu().numpy()
+            lat[f"{kind}{bits}"] = [bool(np.array_equal(got, want)), osgpu.last_coll_path(), dt,
+                                    L.osgpu_last_continuations()]
+            sync()
+        # random entry delays on every member
+        rng = random.Random(77 + rank)
+        jit = {"calls": 0, "exact": 0, "paths": [], "continuations": 0}
+        for k in range(int(os.environ.get("MP_JITTER_CALLS", "120"))):
+            t, op = (("int", "sum"), ("double", "sum"), ("float", "min"))[k % 3]
+            m = (1000, 65536, 4099)[k % 3]
+            s_ = np.dtype(O.NP_DTYPE[t]).itemsize
+            src = O.team_inputs(t, world, m, 0x7700 + k, "wide")
+            want = O.to_all(t, op, src)[rank]
+            toff = (m * s_ + 4095) // 4096 * 4096
+            put(0, src[rank])
+            torch.cuda.synchronize()
+            sync()
+            time.sleep(rng.random() * 0.002)
+            getattr(L, f"shmem_{t}_{op}_to_all")(dev0 + toff, dev0, m, 0, 0, world, wrk, psync)
+            got = heap[toff:toff + m * s_].cpu().numpy()
+            jit["calls"] += 1
+            jit["exact"] += bool(np.array_equal(got, want.view(np.uint8).reshape(-1)))
+            if osgpu.last_path() not in jit["paths"]:
+                jit["paths"].append(osgpu.last_path())
+            jit["continuations"] += L.osgpu_last_continuations()
+        res["late"], res["jitter"] = lat, jit
     if mode == "collgolden":
         import hashlib
         from support import coll_cases as CC
@@ -563,7 +644,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm"):
+            "timeout", "vmm", "late"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -616,7 +697,7 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
-    if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout"):
+    if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout", "late"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "vmm":
         res.update(vmm_heap_mode(L, PES, rank, world))
