@@ -326,6 +326,13 @@ def device_heap_modes(L, PES, mode, rank, world):
         lat = {}
         L.osgpu_last_continuations.restype = ctypes.c_int
         n = 4099
+        # the set's flag areas are made by the first fused call (a collective
+        # setup with host barriers): make them before anyone is late
+        put(0, np.arange(n, dtype=np.int32))
+        torch.cuda.synchronize()
+        sync()
+        L.shmem_int_sum_to_all(dev0 + 65536, dev0, n, 0, 0, world, wrk, psync)
+        sync()
         for ci, (t, op, path) in enumerate((("int", "sum", osgpu.PATH_AUTO),
                                             ("double", "sum", osgpu.PATH_AUTO),
                                             ("float", "prod", osgpu.PATH_PULL),
