@@ -111,6 +111,45 @@ def cpu_baseline(n):
                        f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
 
 
+def cpu_baselines_configs():
+    """BASELINE.md's CPU-baseline plan beyond config 2: the reference's loop
+    shape (oracle_reduce.c: copy, barrier, 64-element getmem chunks, one
+    indirect call per element, barrier; src/reductions.c:79-113), one pinned
+    pthread per PE, on bounded samples of
+      config 3  long and/or/xor, 2 PEs, nreduce = 32 Mi (256 MiB per array):
+                the full size;
+      config 5  float min/max/prod, 8 PEs on 8 cores, a 32 Mi-element sample
+                of the 128 Mi per PE (the loop is linear in nreduce);
+      config 4  double sum, 8 PEs on 8 cores, a 64 Mi-element sample of the
+                1 Gi per PE (16x smaller: at full size 128 GiB of host arrays
+                and ~16x this time per call).
+    Rates: per-PE algbw nreduce*s/t and the fused-convention P*(P+1)*n*s/t
+    (every PE's K = P inputs + 1 output)."""
+    import oracle as O
+    out = {"host_nproc": os.cpu_count(), "kind": "port",
+           "note": "oracle/oracle_reduce.c reference loop shape, pthreads pinned to cores "
+                   "0..P-1, median after 1 warm-up"}
+    plans = (("config3", "long", ("and", "or", "xor"), 2, 32 << 20, "bits", 3),
+             ("config5", "float", ("min", "max", "prod"), 8, 32 << 20, "unit12", 1),
+             ("config4", "double", ("sum",), 8, 64 << 20, "unit12", 1))
+    for name, t, ops, P, n, dist, reps in plans:
+        try:
+            src = O.team_inputs(t, P, n, 0xC0 + P, dist)
+            es = src[0].dtype.itemsize
+            res = {"pes": P, "cores": P, "nreduce_sample": n}
+            for op in ops:
+                sec = O.cpu_baseline(t, op, src, reps=reps, pin=True)
+                res[op] = {"ms_per_call": sec * 1e3, "GiBs_per_PE": n * es / sec / GIB,
+                           "GiBs_fused_convention": P * (P + 1) * n * es / sec / GIB}
+            out[name] = res
+            del src
+        except Exception as e:  # report, never hide
+            out[name] = {"error": repr(e)[:200]}
+    out["config5"]["full_nreduce"] = 128 << 20
+    out["config4"]["full_nreduce"] = 1 << 30
+    return out
+
+
 def _timer_sig(pet):
     pet.pet_time_to_all.restype = ctypes.c_double
     pet.pet_time_to_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -482,6 +521,7 @@ def bench_single(args):
             res["small_call"] = {"error": repr(e)}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_n)
+        res["cpu_baseline_configs"] = cpu_baselines_configs()
     print(json.dumps(res), flush=True)
 
 

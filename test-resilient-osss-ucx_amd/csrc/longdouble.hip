@@ -200,34 +200,57 @@ struct LdTeam {
     unsigned char *dst[kMaxTeam];
 };
 
-// owner-computes form (team.hip): every PE's own fold order, P^2 soft ops;
-// P is a template parameter so the P inputs stay in registers
-template <int OP, int P>
+// owner-computes form (team.hip): every PE's own fold order, P(P-1) soft
+// ops per element; P is a template parameter so the P inputs stay in
+// registers.  x87 add and mul are commutative bit for bit (same rounding of
+// the same exact value; nan_pick is symmetric, x87.hpp), so member 1's fold
+// x1+x0+x2+... equals member 0's x0+x1+x2+...: sum and prod compute it once
+// (P-2 fewer soft ops).  min/max select by position and are not shared.
+// VEC: 16-byte aligned arrays (the x86-64 layout), one dwordx4 per element.
+template <int OP, int P, bool VEC>
 __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
 {
+    constexpr bool kCommutes = OP == 0 || OP == 1;
     const size_t stride = (size_t) gridDim.x * blockDim.x;
     for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         X80 x[P];
 #pragma unroll
-        for (int p = 0; p < P; p++) x[p] = load(a.src[p] + 16 * i);
+        for (int p = 0; p < P; p++)
+            x[p] = VEC ? unpack(__builtin_nontemporal_load(
+                             reinterpret_cast<const u64x2 *>(a.src[p]) + i))
+                       : load(a.src[p] + 16 * i);
+        X80 r0 = x[0];
 #pragma unroll
         for (int q = 0; q < P; q++) {
-            X80 acc = x[q];
+            X80 acc;
+            if (q == 1 && kCommutes) {
+                acc = r0;
+            } else {
+                acc = x[q];
 #pragma unroll
-            for (int j = 0; j < P; j++)
-                if (j != q) acc = apply<OP>(acc, x[j]);
-            store(a.dst[q] + 16 * i, acc);
+                for (int j = 0; j < P; j++)
+                    if (j != q) acc = apply<OP>(acc, x[j]);
+                if (q == 0) r0 = acc;
+            }
+            if (VEC)
+                __builtin_nontemporal_store(pack(acc), reinterpret_cast<u64x2 *>(a.dst[q]) + i);
+            else
+                store(a.dst[q] + 16 * i, acc);
         }
     }
 }
 
 template <int OP>
-hipError_t ld_team_launch(int P, const LdTeam &a, size_t n, unsigned blocks, hipStream_t s)
+hipError_t ld_team_launch(int P, bool vec, const LdTeam &a, size_t n, unsigned blocks,
+                          hipStream_t s)
 {
     switch (P) {
 #define LDT(PP)                                                                \
     case PP:                                                                   \
-        hipLaunchKernelGGL((ld_team_kernel<OP, PP>), dim3(blocks), dim3(256), 0, s, a, n); \
+        if (vec)                                                               \
+            hipLaunchKernelGGL((ld_team_kernel<OP, PP, true>), dim3(blocks), dim3(256), 0, s, a, n); \
+        else                                                                   \
+            hipLaunchKernelGGL((ld_team_kernel<OP, PP, false>), dim3(blocks), dim3(256), 0, s, a, n); \
         return hipGetLastError();
         LDT(2) LDT(3) LDT(4) LDT(5) LDT(6) LDT(7) LDT(8)
 #undef LDT
@@ -242,18 +265,20 @@ hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *
 {
     if (P < 2 || P > kMaxTeam) return hipErrorInvalidValue;
     x87::LdTeam a;
+    bool vec = true;
     for (int p = 0; p < P; p++) {
         a.src[p] = (const unsigned char *) srcs[p];
         a.dst[p] = (unsigned char *) dsts[p];
         if ((((uintptr_t) srcs[p]) | ((uintptr_t) dsts[p])) & 7) return hipErrorInvalidValue;
+        vec = vec && ((((uintptr_t) srcs[p]) | ((uintptr_t) dsts[p])) & 15) == 0;
     }
     size_t blocks = (n + 255) / 256;
     blocks = blocks > 16384 ? 16384 : (blocks ? blocks : 1);
     switch (op) {
-    case 0: return x87::ld_team_launch<0>(P, a, n, (unsigned) blocks, s);
-    case 1: return x87::ld_team_launch<1>(P, a, n, (unsigned) blocks, s);
-    case 5: return x87::ld_team_launch<5>(P, a, n, (unsigned) blocks, s);
-    case 6: return x87::ld_team_launch<6>(P, a, n, (unsigned) blocks, s);
+    case 0: return x87::ld_team_launch<0>(P, vec, a, n, (unsigned) blocks, s);
+    case 1: return x87::ld_team_launch<1>(P, vec, a, n, (unsigned) blocks, s);
+    case 5: return x87::ld_team_launch<5>(P, vec, a, n, (unsigned) blocks, s);
+    case 6: return x87::ld_team_launch<6>(P, vec, a, n, (unsigned) blocks, s);
     }
     return hipErrorInvalidValue;
 }

@@ -95,8 +95,92 @@ OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
     return X80{hi, (sign << 15) | e};
 }
 
+// add() of two NORMAL operands (0 < biased exponent < 0x7fff, J set), the
+// case every soft-float add of ordinary data takes: the same exact-then-round
+// computation as the general path below, on 64-bit halves instead of 128-bit
+// shifts and counts (the general path's variable u128 shifts cost most of a
+// long double team kernel's VALU time).  Bit-identical by construction
+// (same aligned operand, same sticky, same rounding) and by test
+// (tests/test_x87_softfloat.py compiles this header for the host).
+OSGPU_HD inline X80 add_normal(X80 a, X80 b, int Ea, int Eb)
+{
+    uint32_t sa = (a.se >> 15) & 1, sb = (b.se >> 15) & 1;
+    uint64_t ma = a.m, mb = b.m;
+    if (Eb > Ea || (Eb == Ea && mb > ma)) {   // order by magnitude: |a| >= |b|
+        const uint64_t tm = ma; ma = mb; mb = tm;
+        const int te = Ea; Ea = Eb; Eb = te;
+        const uint32_t ts = sa; sa = sb; sb = ts;
+    }
+    const int d = Ea - Eb;
+    // |b| < 2^-65 ulp(a) scale: b lies below the rounding bit and cannot move
+    // the RNE result of a +- b away from a (a's significand >= 2^63: after a
+    // subtraction the borrow is rounded back up)
+    if (d >= 66) return X80{ma, (sa << 15) | (uint32_t) Ea};
+    // B = mb * 2^-d as 64.64 fixed point (bh . bl), the sticky bit of what
+    // falls below bl ORed into bl's last bit (only d = 65 drops a bit)
+    uint64_t bh, bl;
+    if (d == 0) {
+        bh = mb;
+        bl = 0;
+    } else if (d < 64) {
+        bh = mb >> d;
+        bl = mb << (64 - d);
+    } else if (d == 64) {
+        bh = 0;
+        bl = mb;
+    } else {
+        bh = 0;
+        bl = (mb >> 1) | (mb & 1);
+    }
+    int E = Ea;
+    uint64_t hi, lo;
+    if (sa == sb) {
+        lo = bl;
+        hi = ma + bh;
+        if (hi < ma) {                        // carry out of bit 127
+            lo = (lo >> 1) | (hi << 63) | (lo & 1);
+            hi = (hi >> 1) | (1ull << 63);
+            E += 1;
+        }
+    } else {
+        lo = 0 - bl;
+        hi = ma - bh - (bl != 0 ? 1 : 0);
+        if ((hi | lo) == 0) return X80{0, 0};  // exact cancellation: +0 (RNE)
+    }
+    // normalise (bit 127 set)
+    if (!(hi >> 63)) {
+        if (hi) {
+            const int lz = __builtin_clzll(hi);
+            hi = (hi << lz) | (lo >> (64 - lz));
+            lo <<= lz;
+            E -= lz;
+        } else {
+            const int lz = __builtin_clzll(lo);
+            hi = lo << lz;
+            lo = 0;
+            E -= 64 + lz;
+        }
+    }
+    if (E < 1) return round_pack(sa, E, ((u128) hi << 64) | lo);  // gradual underflow
+    // round to nearest even at bit 64
+    if ((lo >> 63) && ((lo << 1) != 0 || (hi & 1))) {
+        hi += 1;
+        if (hi == 0) {
+            hi = 1ull << 63;
+            E += 1;
+        }
+    }
+    if (E >= (int) kEmax) return X80{1ull << 63, (sa << 15) | kEmax};  // overflow -> inf
+    return X80{hi, (sa << 15) | (uint32_t) E};
+}
+
 OSGPU_HD inline X80 add(X80 a, X80 b)
 {
+    {
+        const uint32_t ea = a.se & kEmax, eb = b.se & kEmax;
+        if (ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63))
+            return add_normal(a, b, (int) ea, (int) eb);
+    }
     const Cls ca = classify(a), cb = classify(b);
     if (ca == C_BAD || cb == C_BAD) return defnan();
     if (is_nan(ca) || is_nan(cb)) return nan_pick(a, ca, b, cb);

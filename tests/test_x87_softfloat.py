@@ -86,3 +86,45 @@ def test_cancellation(x87):
     k = O.splitmix64(3, 100_000).astype(np.longdouble) / np.longdouble(2.0 ** 64)
     y = -x * (np.longdouble(1) + np.longdouble(2.0) ** -60 * k)
     check(x87, x, y, use_ref=O.ref_lib() is not None)
+
+
+def _pairs(where, n=60_000):
+    r = O.splitmix64(77, 4 * n).reshape(4, n)
+    base_e = {"unit": 16383, "underflow": 3, "overflow": 0x7FFE - 1}[where]
+    diffs = np.array([0, 1, 2, 3, 62, 63, 64, 65, 66, 67, 70, 120, 200], np.int64)
+    d = diffs[r[0] % np.uint64(diffs.size)]
+    ea = np.full(n, base_e, np.int64) + (r[1] % np.uint64(3)).astype(np.int64) - 1
+    eb = np.clip(ea - d, 1, 0x7FFE)
+    # significands: random, or 2^63 + small, or 2^64 - small (seams of the
+    # borrow / carry cases)
+    kind = r[2] % np.uint64(3)
+    small = r[3] & np.uint64(0xFF)
+    top = np.uint64(1 << 63)
+    ma = np.where(kind == 0, r[2] | top, np.where(kind == 1, top + small,
+                                                  np.uint64((1 << 64) - 1) - small))
+    mb = np.where(kind == 2, r[3] | top, np.where(kind == 1, np.uint64((1 << 64) - 1) - small,
+                                                  top + small))
+    sa = (r[1] >> np.uint64(7)) & np.uint64(1)
+    sb = (r[1] >> np.uint64(9)) & np.uint64(1)
+
+    def pack(m, e, s):
+        arr = np.zeros((n, 16), np.uint8)
+        arr[:, :8] = m.astype(np.uint64).view(np.uint8).reshape(n, 8)
+        se = (e.astype(np.uint64) | (s << np.uint64(15))).astype(np.uint16)
+        arr[:, 8:10] = se.view(np.uint8).reshape(n, 2)
+        return arr.reshape(-1).view(np.longdouble)
+    return pack(ma, ea, sa), pack(mb, eb, sb)
+
+
+@pytest.mark.parametrize("where", ["unit", "underflow", "overflow"])
+def test_aligned_operand_boundaries(x87, where):
+    """The normal-operand fast path of x87 add (x87.hpp add_normal): exponent
+    differences around the 64-bit shift seams (0-3, 62-67, 70, 120, 200),
+    significands next to powers of two (borrow / carry / renormalise cases),
+    both signs, near 1, near the underflow threshold (results on the denormal
+    grid) and near overflow -- bit-exact against the host's x87, both operand
+    orders."""
+    for w in (where,):
+        a, b = _pairs(w)
+        check(x87, a, b, use_ref=O.ref_lib() is not None)
+        check(x87, b, a, use_ref=O.ref_lib() is not None)
