@@ -104,74 +104,64 @@ OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
 // (tests/test_x87_softfloat.py compiles this header for the host).
 OSGPU_HD inline X80 add_normal(X80 a, X80 b, int Ea, int Eb)
 {
-    uint32_t sa = (a.se >> 15) & 1, sb = (b.se >> 15) & 1;
-    uint64_t ma = a.m, mb = b.m;
-    if (Eb > Ea || (Eb == Ea && mb > ma)) {   // order by magnitude: |a| >= |b|
-        const uint64_t tm = ma; ma = mb; mb = tm;
-        const int te = Ea; Ea = Eb; Eb = te;
-        const uint32_t ts = sa; sa = sb; sb = ts;
+    // Written without data-dependent branches (selects only) except the rare
+    // underflow exit: the lanes of a wave holding different signs, exponent
+    // gaps and normalisation shifts then run ONE instruction stream instead
+    // of every branch in turn.
+    // order by magnitude: |A| >= |B|
+    const bool swap = Eb > Ea || (Eb == Ea && b.m > a.m);
+    const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
+    const int EA = swap ? Eb : Ea;
+    const uint32_t sign = ((swap ? b.se : a.se) >> 15) & 1;
+    const bool same = ((a.se ^ b.se) & 0x8000u) == 0;
+    const int d = EA - (swap ? Ea : Eb);  // >= 0
+    // B = mb * 2^-d as 64.64 fixed point (bh . bl) with the sticky bit of
+    // what falls below bl ORed into bl's last bit (only d = 65 drops a bit;
+    // d >= 66 is handled at the end: |B| is below the rounding bit)
+    const int dc = d < 63 ? d : 63;
+    const uint64_t bh = d < 64 ? (mb >> dc) : 0;
+    const uint64_t bl_in = ((mb << (63 - dc)) << 1);  // mb << (64 - d), 0 < d < 64
+    const uint64_t bl = d == 0 ? 0 : d < 64 ? bl_in : d == 64 ? mb : ((mb >> 1) | (mb & 1));
+    // exact A + B or A - B (A's low half is zero)
+    const uint64_t hs = ma + bh;
+    const bool c = same && hs < ma;       // carry out of bit 127
+    uint64_t hi = same ? hs : ma - bh - (bl != 0 ? 1 : 0);
+    uint64_t lo = same ? bl : 0 - bl;
+    const bool zero = !same && (hi | lo) == 0;  // exact cancellation: +0 (RNE)
+    int E = EA;
+    {
+        const uint64_t lo_c = (lo >> 1) | (hi << 63) | (lo & 1);
+        hi = c ? ((hi >> 1) | (1ull << 63)) : hi;
+        lo = c ? lo_c : lo;
+        E += c ? 1 : 0;
     }
-    const int d = Ea - Eb;
-    // |b| < 2^-65 ulp(a) scale: b lies below the rounding bit and cannot move
-    // the RNE result of a +- b away from a (a's significand >= 2^63: after a
-    // subtraction the borrow is rounded back up)
-    if (d >= 66) return X80{ma, (sa << 15) | (uint32_t) Ea};
-    // B = mb * 2^-d as 64.64 fixed point (bh . bl), the sticky bit of what
-    // falls below bl ORed into bl's last bit (only d = 65 drops a bit)
-    uint64_t bh, bl;
-    if (d == 0) {
-        bh = mb;
-        bl = 0;
-    } else if (d < 64) {
-        bh = mb >> d;
-        bl = mb << (64 - d);
-    } else if (d == 64) {
-        bh = 0;
-        bl = mb;
-    } else {
-        bh = 0;
-        bl = (mb >> 1) | (mb & 1);
+    // normalise: shift left by lz (0..127) so bit 127 is set
+    const int lzh = hi ? __builtin_clzll(hi) : 64;
+    const int lzl = lo ? __builtin_clzll(lo) : 64;
+    const int lz = hi ? lzh : 64 + lzl;
+    {
+        const int l1 = lz & 63;
+        const uint64_t carry_in = l1 ? ((lo >> 1) >> (63 - l1)) : 0;  // lo >> (64 - l1)
+        const uint64_t hi_a = (hi << l1) | carry_in, lo_a = lo << l1;
+        hi = lz < 64 ? hi_a : lo_a;
+        lo = lz < 64 ? lo_a : 0;
+        E -= lz;
     }
-    int E = Ea;
-    uint64_t hi, lo;
-    if (sa == sb) {
-        lo = bl;
-        hi = ma + bh;
-        if (hi < ma) {                        // carry out of bit 127
-            lo = (lo >> 1) | (hi << 63) | (lo & 1);
-            hi = (hi >> 1) | (1ull << 63);
-            E += 1;
-        }
-    } else {
-        lo = 0 - bl;
-        hi = ma - bh - (bl != 0 ? 1 : 0);
-        if ((hi | lo) == 0) return X80{0, 0};  // exact cancellation: +0 (RNE)
-    }
-    // normalise (bit 127 set)
-    if (!(hi >> 63)) {
-        if (hi) {
-            const int lz = __builtin_clzll(hi);
-            hi = (hi << lz) | (lo >> (64 - lz));
-            lo <<= lz;
-            E -= lz;
-        } else {
-            const int lz = __builtin_clzll(lo);
-            hi = lo << lz;
-            lo = 0;
-            E -= 64 + lz;
-        }
-    }
-    if (E < 1) return round_pack(sa, E, ((u128) hi << 64) | lo);  // gradual underflow
+    if (!zero && d < 66 && E < 1)
+        return round_pack(sign, E, ((u128) hi << 64) | lo);  // gradual underflow (rare)
     // round to nearest even at bit 64
-    if ((lo >> 63) && ((lo << 1) != 0 || (hi & 1))) {
-        hi += 1;
-        if (hi == 0) {
-            hi = 1ull << 63;
-            E += 1;
-        }
-    }
-    if (E >= (int) kEmax) return X80{1ull << 63, (sa << 15) | kEmax};  // overflow -> inf
-    return X80{hi, (sa << 15) | (uint32_t) E};
+    const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
+    uint64_t hr = hi + (up ? 1 : 0);
+    const bool wrap = up && hr == 0;      // carried out of 64 bits
+    hr = wrap ? (1ull << 63) : hr;
+    E += wrap ? 1 : 0;
+    const bool inf = E >= (int) kEmax;
+    X80 r;
+    r.m = inf ? (1ull << 63) : hr;
+    r.se = (sign << 15) | (inf ? kEmax : (uint32_t) E);
+    if (zero) r = X80{0, 0};
+    if (d >= 66) r = X80{ma, (sign << 15) | (uint32_t) EA};
+    return r;
 }
 
 OSGPU_HD inline X80 add(X80 a, X80 b)

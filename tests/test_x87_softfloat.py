@@ -128,3 +128,20 @@ def test_aligned_operand_boundaries(x87, where):
         a, b = _pairs(w)
         check(x87, a, b, use_ref=O.ref_lib() is not None)
         check(x87, b, a, use_ref=O.ref_lib() is not None)
+
+
+def test_equal_and_opposite_operands(x87):
+    """a + a (carry out of the significand at every exponent, up to overflow)
+    and a + (-a) (exact cancellation to +0), normal, denormal and special
+    encodings alike."""
+    a = np.concatenate([raw_random(20_000, 31, m) for m in ("normal", "near", "low", "high",
+                                                             "any")])
+    raw = O.value_bytes(a).reshape(-1, 10).copy()
+    raw[::2, :7] = 0            # every other significand a power of two (2^63):
+    raw[::2, 7] = 0x80          # a + a carries out of the 64 bits exactly
+    a = O.from_value_bytes("longdouble", raw.reshape(-1))
+    neg = O.value_bytes(a).reshape(-1, 10).copy()
+    neg[:, 9] ^= 0x80
+    b = O.from_value_bytes("longdouble", neg.reshape(-1))
+    check(x87, a, a, use_ref=O.ref_lib() is not None)
+    check(x87, a, b, use_ref=O.ref_lib() is not None)

@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${KEXPR:+-k "$KEXPR"} ${PYTEST_ARGS} ;;
+    ldpre) OSGPU_LIB_PATH=tools/ldvariant/libosgpu_pre.so step ldpre 300 python -u tools/ld_team_rate.py ;;
     ldrate) step ldrate 300 python -u tools/ld_team_rate.py &&
             TR_TYPE=longdouble step ldcall 300 python -u tools/team_rate.py $((8<<20)) ;;
     nsprobe) step nsprobe 300 python -u tools/ns_probe.py ${NS_ARGS} ;;
