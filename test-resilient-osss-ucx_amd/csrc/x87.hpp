@@ -95,81 +95,64 @@ OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
     return X80{hi, (sign << 15) | e};
 }
 
-// add() of two NORMAL operands (0 < biased exponent < 0x7fff, J set), the
-// case every soft-float add of ordinary data takes: the same exact-then-round
-// computation as the general path below, on 64-bit halves instead of 128-bit
-// shifts and counts (the general path's variable u128 shifts cost most of a
-// long double team kernel's VALU time).  Bit-identical by construction
-// (same aligned operand, same sticky, same rounding) and by test
+// add() of two NORMAL operands (0 < biased exponent < 0x7fff, J set) whose
+// exponents differ by less than 64 and whose result stays normal -- what
+// every soft-float add of ordinary data is: the same exact-then-round
+// computation as the general path below, on 64-bit halves, with the few
+// data-dependent choices (swap, add or subtract, carry or renormalise, round
+// up) made by selects so the lanes of a wave run one instruction stream.
+// Everything else (gaps of 64+, cancellation into the low half, underflow,
+// specials) returns false and takes the general path.  Bit-identical by
+// construction (same aligned operand, same rounding) and by test
 // (tests/test_x87_softfloat.py compiles this header for the host).
-OSGPU_HD inline X80 add_normal(X80 a, X80 b, int Ea, int Eb)
+OSGPU_HD inline bool add_normal(X80 a, X80 b, uint32_t ea, uint32_t eb, X80 *r)
 {
-    // Written without data-dependent branches (selects only) except the rare
-    // underflow exit: the lanes of a wave holding different signs, exponent
-    // gaps and normalisation shifts then run ONE instruction stream instead
-    // of every branch in turn.
-    // order by magnitude: |A| >= |B|
-    const bool swap = Eb > Ea || (Eb == Ea && b.m > a.m);
+    const bool swap = eb > ea || (eb == ea && b.m > a.m);  // |A| >= |B|
     const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
-    const int EA = swap ? Eb : Ea;
+    const int EA = (int) (swap ? eb : ea);
+    const int d = EA - (int) (swap ? ea : eb);
     const uint32_t sign = ((swap ? b.se : a.se) >> 15) & 1;
+    if (d >= 66) {  // |B| below the rounding bit: the RNE result is A
+        *r = X80{ma, (sign << 15) | (uint32_t) EA};
+        return true;
+    }
+    if (d >= 64) return false;
     const bool same = ((a.se ^ b.se) & 0x8000u) == 0;
-    const int d = EA - (swap ? Ea : Eb);  // >= 0
-    // B = mb * 2^-d as 64.64 fixed point (bh . bl) with the sticky bit of
-    // what falls below bl ORed into bl's last bit (only d = 65 drops a bit;
-    // d >= 66 is handled at the end: |B| is below the rounding bit)
-    const int dc = d < 63 ? d : 63;
-    const uint64_t bh = d < 64 ? (mb >> dc) : 0;
-    const uint64_t bl_in = ((mb << (63 - dc)) << 1);  // mb << (64 - d), 0 < d < 64
-    const uint64_t bl = d == 0 ? 0 : d < 64 ? bl_in : d == 64 ? mb : ((mb >> 1) | (mb & 1));
-    // exact A + B or A - B (A's low half is zero)
+    // B = mb * 2^-d as 64.64 fixed point, exact for d < 64
+    const uint64_t bh = mb >> d;
+    const uint64_t bl = d ? mb << ((64 - d) & 63) : 0;
     const uint64_t hs = ma + bh;
-    const bool c = same && hs < ma;       // carry out of bit 127
+    const bool c = same && hs < ma;  // carry out of bit 127
     uint64_t hi = same ? hs : ma - bh - (bl != 0 ? 1 : 0);
     uint64_t lo = same ? bl : 0 - bl;
-    const bool zero = !same && (hi | lo) == 0;  // exact cancellation: +0 (RNE)
-    int E = EA;
-    {
-        const uint64_t lo_c = (lo >> 1) | (hi << 63) | (lo & 1);
-        hi = c ? ((hi >> 1) | (1ull << 63)) : hi;
-        lo = c ? lo_c : lo;
-        E += c ? 1 : 0;
-    }
-    // normalise: shift left by lz (0..127) so bit 127 is set
-    const int lzh = hi ? __builtin_clzll(hi) : 64;
-    const int lzl = lo ? __builtin_clzll(lo) : 64;
-    const int lz = hi ? lzh : 64 + lzl;
-    {
-        const int l1 = lz & 63;
-        const uint64_t carry_in = l1 ? ((lo >> 1) >> (63 - l1)) : 0;  // lo >> (64 - l1)
-        const uint64_t hi_a = (hi << l1) | carry_in, lo_a = lo << l1;
-        hi = lz < 64 ? hi_a : lo_a;
-        lo = lz < 64 ? lo_a : 0;
-        E -= lz;
-    }
-    if (!zero && d < 66 && E < 1)
-        return round_pack(sign, E, ((u128) hi << 64) | lo);  // gradual underflow (rare)
+    if (!same && hi == 0) return false;  // cancellation into the low half
+    // renormalise: right by one on a carry, left by lz after a subtraction
+    const int lz = same ? 0 : __builtin_clzll(hi);
+    const uint64_t hr = (hi >> 1) | (1ull << 63), lr = (lo >> 1) | (hi << 63) | (lo & 1);
+    const uint64_t hl = lz ? (hi << lz) | (lo >> ((64 - lz) & 63)) : hi, ll = lo << lz;
+    hi = c ? hr : hl;
+    lo = c ? lr : ll;
+    int E = EA + (c ? 1 : -lz);
+    if (E < 1) return false;  // gradual underflow
     // round to nearest even at bit 64
     const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
-    uint64_t hr = hi + (up ? 1 : 0);
-    const bool wrap = up && hr == 0;      // carried out of 64 bits
-    hr = wrap ? (1ull << 63) : hr;
+    hi += up ? 1 : 0;
+    const bool wrap = up && hi == 0;  // carried out of 64 bits
+    hi = wrap ? (1ull << 63) : hi;
     E += wrap ? 1 : 0;
     const bool inf = E >= (int) kEmax;
-    X80 r;
-    r.m = inf ? (1ull << 63) : hr;
-    r.se = (sign << 15) | (inf ? kEmax : (uint32_t) E);
-    if (zero) r = X80{0, 0};
-    if (d >= 66) r = X80{ma, (sign << 15) | (uint32_t) EA};
-    return r;
+    *r = X80{inf ? (1ull << 63) : hi, (sign << 15) | (inf ? kEmax : (uint32_t) E)};
+    return true;
 }
 
 OSGPU_HD inline X80 add(X80 a, X80 b)
 {
     {
         const uint32_t ea = a.se & kEmax, eb = b.se & kEmax;
-        if (ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63))
-            return add_normal(a, b, (int) ea, (int) eb);
+        X80 r;
+        if (ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63) &&
+            add_normal(a, b, ea, eb, &r))
+            return r;
     }
     const Cls ca = classify(a), cb = classify(b);
     if (ca == C_BAD || cb == C_BAD) return defnan();
