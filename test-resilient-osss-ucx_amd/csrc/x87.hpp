@@ -96,50 +96,49 @@ OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
 }
 
 // The general add: every encoding, exact 128-bit intermediate, one RNE
-// rounding.  Not inlined: a fold of P inputs makes P(P-1) adds, and the
-// rarely taken general path inlined into each of them made a long double
-// team kernel of 24 K instructions, beyond the instruction cache.
+// rounding (below).
 OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b);
 
-// add(): first the case every soft-float add of ordinary data is -- two
-// NORMAL operands (0 < biased exponent < 0x7fff, J set) whose exponents
-// differ by less than 64 (or by 66 and more: the smaller is below the
-// rounding bit and the RNE result is the larger) and whose result stays
-// normal: the same exact-then-round computation as add_general, on 64-bit
-// halves, computed unconditionally with selects (swap, add or subtract,
-// carry or renormalise, round up) so a wave runs ONE instruction stream and
-// takes ONE branch -- to add_general, for whatever the fast form does not
-// cover (gaps of 64 and 65, cancellation into the low half, underflow,
-// zeros, denormals, specials).  Bit-identical by construction (same aligned
-// operand, same rounding) and by test (tests/test_x87_softfloat.py compiles
-// this header for the host).
-OSGPU_HD inline X80 add(X80 a, X80 b)
+// add() of two NORMAL operands (0 < biased exponent < 0x7fff, J set) whose
+// exponents differ by less than 64 (or by 66 and more: the smaller is then
+// below the rounding bit and the RNE result is the larger) and whose result
+// stays normal -- what every soft-float add of ordinary data is: the same
+// exact-then-round computation as add_general, on 64-bit halves, with the
+// data-dependent choices (swap, add or subtract, carry or renormalise, round
+// up) made by selects so the lanes of a wave run one instruction stream.
+// false: not covered (gaps of 64 and 65, cancellation into the low half,
+// underflow) -- add_general takes it.  Bit-identical by construction (same
+// aligned operand, same rounding) and by test (tests/test_x87_softfloat.py
+// compiles this header for the host).
+OSGPU_HD inline bool add_normal(X80 a, X80 b, uint32_t ea, uint32_t eb, X80 *r)
 {
-    const uint32_t ea = a.se & kEmax, eb = b.se & kEmax;
-    const bool normal = ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63);
     const bool swap = eb > ea || (eb == ea && b.m > a.m);  // |A| >= |B|
     const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
-    const uint32_t EA = swap ? eb : ea;
-    const uint32_t d = EA - (swap ? ea : eb);
+    const int EA = (int) (swap ? eb : ea);
+    const int d = EA - (int) (swap ? ea : eb);
     const uint32_t sign = ((swap ? b.se : a.se) >> 15) & 1;
+    if (d >= 66) {
+        *r = X80{ma, (sign << 15) | (uint32_t) EA};
+        return true;
+    }
+    if (d >= 64) return false;
     const bool same = ((a.se ^ b.se) & 0x8000u) == 0;
-    // B = mb * 2^-d as 64.64 fixed point (exact for d < 64)
-    const uint32_t ds = d & 63;
-    const uint64_t bh = mb >> ds;
-    const uint64_t bl = ds ? mb << ((64 - ds) & 63) : 0;
+    // B = mb * 2^-d as 64.64 fixed point, exact for d < 64
+    const uint64_t bh = mb >> d;
+    const uint64_t bl = d ? mb << ((64 - d) & 63) : 0;
     const uint64_t hs = ma + bh;
     const bool c = same && hs < ma;  // carry out of bit 127
     uint64_t hi = same ? hs : ma - bh - (bl != 0 ? 1 : 0);
     uint64_t lo = same ? bl : 0 - bl;
-    const bool low_cancel = !same && hi == 0;
+    if (!same && hi == 0) return false;  // cancellation into the low half
     // renormalise: right by one on a carry, left by lz after a subtraction
-    const int lz = same ? 0 : __builtin_clzll(hi | 1);
+    const int lz = same ? 0 : __builtin_clzll(hi);
     const uint64_t hr = (hi >> 1) | (1ull << 63), lr = (lo >> 1) | (hi << 63) | (lo & 1);
     const uint64_t hl = lz ? (hi << lz) | (lo >> ((64 - lz) & 63)) : hi, ll = lo << lz;
     hi = c ? hr : hl;
     lo = c ? lr : ll;
-    int E = (int) EA + (c ? 1 : -lz);
-    const bool underflow = E < 1;
+    int E = EA + (c ? 1 : -lz);
+    if (E < 1) return false;  // gradual underflow
     // round to nearest even at bit 64
     const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
     hi += up ? 1 : 0;
@@ -147,11 +146,21 @@ OSGPU_HD inline X80 add(X80 a, X80 b)
     hi = wrap ? (1ull << 63) : hi;
     E += wrap ? 1 : 0;
     const bool inf = E >= (int) kEmax;
-    const bool big_gap = d >= 66;
+    *r = X80{inf ? (1ull << 63) : hi, (sign << 15) | (inf ? kEmax : (uint32_t) E)};
+    return true;
+}
+
+// The fast form when it applies, else the general add (out of line: a fold
+// of P inputs makes P(P-1) adds, and the rarely taken general path inlined
+// into each of them made a long double team kernel of 24 K instructions,
+// beyond the instruction cache).
+OSGPU_HD inline X80 add(X80 a, X80 b)
+{
+    const uint32_t ea = a.se & kEmax, eb = b.se & kEmax;
     X80 r;
-    r.m = big_gap ? ma : inf ? (1ull << 63) : hi;
-    r.se = (sign << 15) | (big_gap ? EA : inf ? kEmax : (uint32_t) E);
-    if (normal && (big_gap || (d < 64 && !low_cancel && !underflow))) return r;
+    if (ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63) &&
+        add_normal(a, b, ea, eb, &r))
+        return r;
     return add_general(a, b);
 }
 
