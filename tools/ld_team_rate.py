@@ -24,9 +24,13 @@ dev = torch.device("cuda:0")
 st = torch.cuda.Stream()
 sp = ctypes.c_void_p(st.cuda_stream)
 g = torch.Generator(device=dev).manual_seed(5)
+# LD_ONLY="sum/random/8": one case (e.g. for a PMC pass)
+only = os.environ.get("LD_ONLY")
 for op_name, op in (("sum", 0), ("prod", 1)):
     for dist in ("ones", "random"):
         for P in (2, 4, 8):
+            if only and only != f"{op_name}/{dist}/{P}":
+                continue
             srcs = []
             for p in range(P):
                 v = torch.empty((n, 2), dtype=torch.int64, device=dev)
