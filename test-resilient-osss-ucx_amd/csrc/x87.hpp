@@ -99,7 +99,19 @@ OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
 // rounding (below).
 OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b);
 
-// add() of two NORMAL operands (0 < biased exponent < 0x7fff, J set) whose
+// Unpacked operand of the fast add: significand, biased exponent and sign
+// in their own registers, so a fold that feeds one add's result to the next
+// (and reuses each input P-1 times) does not re-extract them every time.
+struct XU {
+    uint64_t m;
+    uint32_t e;  // biased exponent, 0..0x7fff
+    uint32_t s;  // sign, 0 or 1
+};
+
+OSGPU_HD inline XU unpack_u(X80 x) { return XU{x.m, x.se & kEmax, (x.se >> 15) & 1}; }
+OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s << 15) | x.e}; }
+
+// add of two NORMAL operands (0 < biased exponent < 0x7fff, J set) whose
 // exponents differ by less than 64 (or by 66 and more: the smaller is then
 // below the rounding bit and the RNE result is the larger) and whose result
 // stays normal -- what every soft-float add of ordinary data is: the same
@@ -110,19 +122,19 @@ OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b);
 // underflow) -- add_general takes it.  Bit-identical by construction (same
 // aligned operand, same rounding) and by test (tests/test_x87_softfloat.py
 // compiles this header for the host).
-OSGPU_HD inline bool add_normal(X80 a, X80 b, uint32_t ea, uint32_t eb, X80 *r)
+OSGPU_HD inline bool add_normal(XU a, XU b, XU *r)
 {
-    const bool swap = eb > ea || (eb == ea && b.m > a.m);  // |A| >= |B|
+    const bool swap = b.e > a.e || (b.e == a.e && b.m > a.m);  // |A| >= |B|
     const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
-    const int EA = (int) (swap ? eb : ea);
-    const int d = EA - (int) (swap ? ea : eb);
-    const uint32_t sign = ((swap ? b.se : a.se) >> 15) & 1;
+    const int EA = (int) (swap ? b.e : a.e);
+    const int d = EA - (int) (swap ? a.e : b.e);
+    const uint32_t sign = swap ? b.s : a.s;
     if (d >= 66) {
-        *r = X80{ma, (sign << 15) | (uint32_t) EA};
+        *r = XU{ma, (uint32_t) EA, sign};
         return true;
     }
     if (d >= 64) return false;
-    const bool same = ((a.se ^ b.se) & 0x8000u) == 0;
+    const bool same = a.s == b.s;
     // B = mb * 2^-d as 64.64 fixed point, exact for d < 64
     const uint64_t bh = mb >> d;
     const uint64_t bl = d ? mb << ((64 - d) & 63) : 0;
@@ -146,7 +158,7 @@ OSGPU_HD inline bool add_normal(X80 a, X80 b, uint32_t ea, uint32_t eb, X80 *r)
     hi = wrap ? (1ull << 63) : hi;
     E += wrap ? 1 : 0;
     const bool inf = E >= (int) kEmax;
-    *r = X80{inf ? (1ull << 63) : hi, (sign << 15) | (inf ? kEmax : (uint32_t) E)};
+    *r = XU{inf ? (1ull << 63) : hi, inf ? kEmax : (uint32_t) E, sign};
     return true;
 }
 
@@ -154,15 +166,16 @@ OSGPU_HD inline bool add_normal(X80 a, X80 b, uint32_t ea, uint32_t eb, X80 *r)
 // of P inputs makes P(P-1) adds, and the rarely taken general path inlined
 // into each of them made a long double team kernel of 24 K instructions,
 // beyond the instruction cache).
-OSGPU_HD inline X80 add(X80 a, X80 b)
+OSGPU_HD inline XU add_u(XU a, XU b)
 {
-    const uint32_t ea = a.se & kEmax, eb = b.se & kEmax;
-    X80 r;
-    if (ea - 1u < kEmax - 1u && eb - 1u < kEmax - 1u && ((a.m & b.m) >> 63) &&
-        add_normal(a, b, ea, eb, &r))
+    XU r;
+    if (a.e - 1u < kEmax - 1u && b.e - 1u < kEmax - 1u && ((a.m & b.m) >> 63) &&
+        add_normal(a, b, &r))
         return r;
-    return add_general(a, b);
+    return unpack_u(add_general(pack_u(a), pack_u(b)));
 }
+
+OSGPU_HD inline X80 add(X80 a, X80 b) { return pack_u(add_u(unpack_u(a), unpack_u(b))); }
 
 OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b)
 {
