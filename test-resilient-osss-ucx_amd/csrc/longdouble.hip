@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
             x[p] = VEC ? unpack(__builtin_nontemporal_load(
                              reinterpret_cast<const u64x2 *>(a.src[p]) + i))
                        : load(a.src[p] + 16 * i);
-        // sum: every input unpacked once, the folds run on unpacked values
+        // sum / prod: every input unpacked once, the folds run on unpacked values
         XU u[P];
 #pragma unroll
         for (int p = 0; p < P; p++) u[p] = unpack_u(x[p]);
@@ -229,11 +229,11 @@ __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
             X80 acc;
             if (q == 1 && kCommutes) {
                 acc = r0;
-            } else if (OP == 0) {
+            } else if (OP == 0 || OP == 1) {
                 XU ua = u[q];
 #pragma unroll
                 for (int j = 0; j < P; j++)
-                    if (j != q) ua = add_u(ua, u[j]);
+                    if (j != q) ua = OP == 0 ? add_u(ua, u[j]) : mul_u(ua, u[j]);
                 acc = pack_u(ua);
                 if (q == 0) r0 = acc;
             } else {

@@ -230,7 +230,40 @@ OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b)
     return round_pack(sign, E, S);
 }
 
-OSGPU_HD inline X80 mul(X80 a, X80 b)
+OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b);
+
+// mul of two NORMAL operands whose product stays normal: the exact 128-bit
+// product of two significands with J set lies in [2^126, 2^128), so the
+// renormalising shift is 0 or 1 (a select), then one RNE rounding at bit 64
+// -- the general path's computation without its classification and
+// variable shifts.  Everything else goes to mul_general.
+OSGPU_HD inline XU mul_u(XU a, XU b)
+{
+    if (a.e - 1u < kEmax - 1u && b.e - 1u < kEmax - 1u && ((a.m & b.m) >> 63)) {
+        const u128 P = (u128) a.m * (u128) b.m;
+        uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
+        const bool top = (hi >> 63) != 0;
+        const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
+        hi = top ? hi : h1;
+        lo = top ? lo : l1;
+        // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = S * 2^(E-bias-127)
+        int E = (int) a.e + (int) b.e - kBias + (top ? 1 : 0);
+        if (E >= 1) {
+            const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
+            hi += up ? 1 : 0;
+            const bool wrap = up && hi == 0;
+            hi = wrap ? (1ull << 63) : hi;
+            E += wrap ? 1 : 0;
+            const bool inf = E >= (int) kEmax;
+            return XU{inf ? (1ull << 63) : hi, inf ? kEmax : (uint32_t) E, a.s ^ b.s};
+        }
+    }
+    return unpack_u(mul_general(pack_u(a), pack_u(b)));
+}
+
+OSGPU_HD inline X80 mul(X80 a, X80 b) { return pack_u(mul_u(unpack_u(a), unpack_u(b))); }
+
+OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
 {
     const Cls ca = classify(a), cb = classify(b);
     if (ca == C_BAD || cb == C_BAD) return defnan();
