@@ -26,6 +26,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     ldpmc) export LD_ONLY=sum/random/8 REPS=5
            step ldpmc1 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d gpurun_out/ldpmc1 -o run --output-format csv -- python3 tools/ld_team_rate.py &&
            step ldpmc2 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/ldpmc2 -o run --output-format csv -- python3 tools/ld_team_rate.py ;;
+    xover) step xover 600 python -u tools/crossover.py ;;
     nsprobe) step nsprobe 300 python -u tools/ns_probe.py ${NS_ARGS} ;;
     vmmprobe) step vmmprobe 200 python -u tools/vmm_probe.py 2 ;;
     vmm)   step vmm 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_multiproc.py -k vmm ;;
