@@ -1316,6 +1316,11 @@ int osgpu_last_continuations(void) { return t_continuations; }
 
 const char *osgpu_last_error(void) { return g_err; }
 
-const char *osgpu_version(void) { return "osgpu_reduce 0.1 (gfx950)"; }
+const char *osgpu_version(void) { return "osgpu_reduce 0.2 (gfx950)"; }
+
+#ifndef OSGPU_BUILD_ID
+#define OSGPU_BUILD_ID "unknown"
+#endif
+const char *osgpu_build_id(void) { return OSGPU_BUILD_ID; }
 
 }  // extern "C"

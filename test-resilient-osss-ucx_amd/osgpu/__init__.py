@@ -127,6 +127,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_combine.argtypes = [i, i, vp, vp, i, sz, vp]
     L.osgpu_copy.argtypes = [vp, vp, vp, i, vp]
     L.osgpu_team_combine.argtypes = [i, i, i, vp, vp, sz, vp]
+    L.osgpu_build_id.restype = ctypes.c_char_p
     L.osgpu_has_op.argtypes = [i, i]
     L.osgpu_type_size.argtypes = [i]
     L.osgpu_type_size.restype = sz
@@ -169,6 +170,20 @@ def compare(a: int, b: int, nbytes: int, stream: int | None = None):
     if rc != 0:
         raise RuntimeError(load().osgpu_last_error().decode())
     return bad.value, (None if first.value == (1 << 64) - 1 else first.value)
+
+
+def source_build_id() -> str:
+    """The build id the Makefile would stamp on a library built from the
+    sources in this tree (csrc/Makefile BUILD_ID)."""
+    import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp"))
+                   + glob.glob(os.path.join(CSRC, "*.hpp")), key=os.path.basename)
+    h = hashlib.sha256()
+    for f in files + [HEADER]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def device_view(ptr: int, nbytes: int, dtype=None):
