@@ -333,3 +333,96 @@ def test_config3_bitwise_full_size(torch_cuda):
                   _stream(torch))
     torch.cuda.synchronize()
     assert torch.equal(out, a)
+
+
+def test_heap_create_threads_as_pes(torch_cuda):
+    """osgpu_heap_create when the members are threads of one process (they
+    share each other's range directly, no descriptors): three PEs each make
+    a 24 MiB device heap in the same collective call; double sum (team and
+    pull form), int xor and long double sum run on objects inside the heaps,
+    bit-exact against the oracle's per-PE folds; pSync comes back zeroed
+    (the helper asserts it), and the heaps are destroyed again."""
+    tm = team(True)
+    L = tm.lib
+    P = 3
+    nbytes = 24 << 20
+    bases = {}
+
+    def create(pe):
+        b = ctypes.c_void_p()
+        rc = L.osgpu_heap_create(nbytes, 0, 0, P, tm.psync_ptr(pe), ctypes.byref(b))
+        assert rc == 0, L.osgpu_last_error().decode()
+        bases[pe] = b.value
+
+    tm._on_members(list(range(P)), create)
+    assert len(set(bases.values())) == P
+    views = {pe: osgpu.device_view(bases[pe], nbytes) for pe in range(P)}
+    try:
+        for t, op, n, dist, path in (("double", "sum", 100_003, "wide", osgpu.PATH_AUTO),
+                                     ("double", "sum", 100_003, "wide", osgpu.PATH_PULL),
+                                     ("int", "xor", 777_777, "bits", osgpu.PATH_AUTO),
+                                     ("longdouble", "sum", 4099, "wide", osgpu.PATH_AUTO)):
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            src = O.team_inputs(t, P, n, 0x4EA9, dist)
+            toff = (n * s + 4095) // 4096 * 4096
+            for pe in range(P):
+                raw = np.ascontiguousarray(src[pe]).view(np.uint8).reshape(-1)
+                views[pe][:raw.size].copy_(torch_cuda.from_numpy(raw.copy()).cuda())
+                views[pe][toff:toff + n * s].fill_(0xA5)
+            torch_cuda.cuda.synchronize()
+            L.osgpu_set_path(path)
+            fn = osgpu.to_all(t, op)
+            pwrk = (ctypes.c_byte * 4096)()
+            tm._on_members(list(range(P)), lambda pe: fn(
+                bases[pe] + toff, bases[pe], n, 0, 0, P, ctypes.addressof(pwrk),
+                tm.psync_ptr(pe)))
+            L.osgpu_set_path(osgpu.PATH_AUTO)
+            want = O.to_all(t, op, src)
+            for pe in range(P):
+                torch_cuda.cuda.synchronize()
+                got = views[pe][toff:toff + n * s].cpu().numpy()
+                if t == "longdouble":
+                    got = got.reshape(-1, 16)[:, :10].reshape(-1)
+                assert np.array_equal(got, O.value_bytes(want[pe]).reshape(-1)), (t, op, path, pe)
+                assert tm.last_paths[pe] == ("pull" if path == osgpu.PATH_PULL else "team")
+    finally:
+        torch_cuda.cuda.synchronize()
+        views.clear()
+        for pe in range(P):
+            assert L.osgpu_heap_destroy(ctypes.c_void_p(bases[pe])) == 0
+
+
+@pytest.mark.parametrize("t,op,P", [("double", "sum", 2), ("float", "min", 5), ("int", "prod", 8),
+                                    ("complexd", "prod", 3), ("longdouble", "sum", 8),
+                                    ("longdouble", "prod", 4)])
+@pytest.mark.parametrize("shift", [0, 1])
+def test_team_combine_launcher(torch_cuda, t, op, P, shift):
+    """osgpu_team_combine, the TEAM path's kernel through the C ABI: output q
+    is member q's fold order (src/reductions.c:79-111), bit-exact against
+    the oracle; shift 1 starts every array one element past a 16-B boundary
+    (scalar head and tail around the vector body)."""
+    s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+    n = 70_001
+    src = O.team_inputs(t, P, n, 0x7EA0 + P, "wide")
+    want = O.to_all(t, op, src)
+    nb = n * s + 64
+    dev = torch_cuda.device("cuda:0")
+    ins = [torch_cuda.empty(nb, dtype=torch_cuda.uint8, device=dev) for _ in range(P)]
+    outs = [torch_cuda.full((nb,), 0x5A, dtype=torch_cuda.uint8, device=dev) for _ in range(P)]
+    off = shift * s if t != "longdouble" else 0
+    for p in range(P):
+        raw = np.ascontiguousarray(src[p]).view(np.uint8).reshape(-1)
+        ins[p][off:off + raw.size].copy_(torch_cuda.from_numpy(raw.copy()).to(dev))
+    S = (ctypes.c_void_p * P)(*[x.data_ptr() + off for x in ins])
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() + off for x in outs])
+    torch_cuda.cuda.synchronize()
+    L = osgpu.load()
+    assert L.osgpu_team_combine(osgpu.TYPES.index(t), osgpu.OPS.index(op), P, D, S, n, None) == 0
+    torch_cuda.cuda.synchronize()
+    for q in range(P):
+        got = outs[q][off:off + n * s].cpu().numpy()
+        if t == "longdouble":
+            got = got.reshape(-1, 16)[:, :10].reshape(-1)
+        assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (t, op, P, q)
+        assert (outs[q][:off].cpu().numpy() == 0x5A).all()
+        assert (outs[q][off + n * s:].cpu().numpy() == 0x5A).all()
