@@ -385,15 +385,26 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     for (int i = 0; i < PE_size; i++)
         if (c.pe_at(i) != c.me && msg[i].pid != (long) getpid()) expected++;
     DBG("%s PE %d: layouts read, %d members in other processes", where, c.me, expected);
+    // Serve my descriptors to every member in another process until all of
+    // them have connected, or until every member has finished importing (the
+    // status barrier below: a member that failed may never connect), or a
+    // time bound passes.
     std::atomic<int> served{0};
+    std::atomic<bool> stop{false};
     std::thread server;
     if (lfd >= 0 && expected > 0 && mine->bytes > 0) {
         server = std::thread([&, lfd, expected] {
-            for (int k = 0; k < expected; k++) {
+            int waited_ms = 0;
+            for (int k = 0; k < expected && !stop.load() && waited_ms < kSetupTimeoutMs;) {
                 pollfd p = {lfd, POLLIN, 0};
-                if (poll(&p, 1, kSetupTimeoutMs) <= 0) return;
+                const int r = poll(&p, 1, 100);
+                if (r < 0 && errno != EINTR) return;
+                if (r <= 0) {
+                    waited_ms += 100;
+                    continue;
+                }
                 const int s = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
-                if (s < 0) return;
+                if (s < 0) continue;
                 DBG("osgpu_heap_create: serving connection %d", k);
                 if (send_fds(s, fds)) {
                     char ack;
@@ -401,6 +412,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
                     served.fetch_add(1);
                 }
                 close(s);
+                k++;
             }
         });
     }
@@ -417,6 +429,11 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             continue;
         }
         const int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        if (s >= 0) {  // a member that stopped serving must not hang this one
+            timeval tv = {kSetupTimeoutMs / 1000, 0};
+            setsockopt(s, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+            setsockopt(s, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+        }
         sockaddr_un a;
         socklen_t al;
         sock_name(msg[i].pid, msg[i].nonce, &a, &al);
@@ -467,15 +484,15 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         DBG("%s PE %d: PE %d's heap mapped at %p", where, c.me, pe, (void *) m.base);
         H->peers.push_back(m);
     }
-    if (server.joinable()) server.join();
-    if (served.load() != expected && mine->bytes > 0) ok = false;
-    if (lfd >= 0) close(lfd);
-    for (int fd : fds) close(fd);
-
-    // every member's verdict
-    DBG("%s PE %d: served %d of %d, ok=%d", where, c.me, served.load(), expected, (int) ok);
+    // every member's verdict; after this barrier every member has finished
+    // importing, so no one connects any more: the server can stop
     mine->status = ok ? 1 : 2;
     barrier(c);
+    stop.store(true);
+    if (server.joinable()) server.join();
+    if (lfd >= 0) close(lfd);
+    for (int fd : fds) close(fd);
+    DBG("%s PE %d: served %d of %d, ok=%d", where, c.me, served.load(), expected, (int) ok);
     bool all_ok = ok;
     for (int i = 0; i < PE_size; i++) {
         const int pe = c.pe_at(i);

@@ -115,11 +115,20 @@ def vmm_heap_mode(L, PES, rank, world):
     psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
     PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     base_p = ctypes.c_void_p()
+    # a member that cannot make its heap (1 PiB): every member gets the same
+    # failure, promptly, and nothing is left registered
+    import time as _time
+    t0 = _time.perf_counter()
+    rc = L.osgpu_heap_create(1 << 50 if rank == 1 else 64 << 20, 0, 0, world, psync,
+                             ctypes.byref(base_p))
+    fail_s = _time.perf_counter() - t0
+    assert rc != 0, "a heap of 1 PiB on one member must fail everywhere"
+    assert not any(ctypes.string_at(psync, 512)), "pSync not reset"
     rc = L.osgpu_heap_create(heap_bytes, 0, 0, world, psync, ctypes.byref(base_p))
     assert rc == 0, (rc, L.osgpu_last_error().decode())
     assert not any(ctypes.string_at(psync, 512)), "pSync not reset"
     base = base_p.value
-    res = {"heap_bytes": heap_bytes, "nbytes": nbytes}
+    res = {"heap_bytes": heap_bytes, "nbytes": nbytes, "failed_create_s": fail_s}
     # every member's heap is reachable at base + offset on every PE
     for pe in range(world):
         peer = L.osgpu_heap_translate(base + off_t, rank, pe)
