@@ -11,6 +11,10 @@ Not part of the product; one MI355X.
   team    the TEAM path's kernel (team_vec_kernel<double,SUM,2>) over all n,
           one launch, and as the 2-PE call issues it (two launches of n/2 on
           two streams), vs the combine; bytes 4*n*8 vs 3*n*8
+  split   the 128 Mi combine as k back-to-back launches over n/k chunks
+          (k = 1..16) on one stream, timed as a group
+  alt     2^26 / 2^27 combines alternating between two array sets per launch
+          (no chance of reuse from the previous launch's arrays)
 Every figure: median of REPS launches timed with HIP events on the launch
 stream; JSON lines on stdout and in gpurun_out/ns_probe.jsonl.
 usage: python tools/ns_probe.py [alloc carve flush team]"""
@@ -156,6 +160,48 @@ def team():
     med, best = time_launches(combine_launcher(a.data_ptr(), b.data_ptr(), o0.data_ptr(), n))
     emit({"probe": "combine_same_arrays", "n": n, "us": med * 1e6,
           "frac": 3 * n * 8 / med / 8e12, "best_frac": 3 * n * 8 / best / 8e12})
+
+
+def split():
+    n = 128 << 20
+    a = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1, 2)
+    b = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1, 2)
+    o = torch.empty(n, dtype=torch.float64, device=dev)
+    for k in (1, 2, 4, 8, 16):
+        c = n // k
+        gos = [combine_launcher(a.data_ptr() + i * c * 8, b.data_ptr() + i * c * 8,
+                                o.data_ptr() + i * c * 8, c) for i in range(k)]
+
+        def group():
+            for g in gos:
+                g()
+        o.zero_()
+        med, best = time_launches(group)
+        assert torch.equal(o, a + b)
+        emit({"probe": "split", "n": n, "k": k, "us": med * 1e6,
+              "frac": 3 * n * 8 / med / 8e12, "best_frac": 3 * n * 8 / best / 8e12})
+    del a, b, o
+    torch.cuda.empty_cache()
+
+
+def alt():
+    for lg in (26, 27):
+        n = 1 << lg
+        sets = []
+        for _ in range(2):
+            sets.append([torch.empty(n, dtype=torch.float64, device=dev).uniform_(1, 2)
+                         for _ in range(3)])
+        gos = [combine_launcher(x.data_ptr(), y.data_ptr(), z.data_ptr(), n) for x, y, z in sets]
+        flip = [0]
+
+        def go():
+            gos[flip[0]]()
+            flip[0] ^= 1
+        med, best = time_launches(go)
+        emit({"probe": "alt", "n": n, "us": med * 1e6,
+              "frac": 3 * n * 8 / med / 8e12, "best_frac": 3 * n * 8 / best / 8e12})
+        del sets
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
