@@ -20,12 +20,15 @@ N = 1 (default) -- BASELINE config 2: nreduce = 64 Mi doubles, 1 MI355X,
 N > 1 (torchrun, one process per GPU) -- one PE per GPU, every PE calls
   shmem_double_sum_to_all(nreduce = 64 Mi per PE) over all N PEs (weak
   scaling: per-GPU data fixed).  Primary path: the exact owner-computes team
-  kernel over IPC-mapped peer heaps (xGMI); PE services from an intra-node
-  shared-memory runtime (tests/support/pe_shm.c); a sampled bit-exact parity
-  check against the oracle is reported.  value = steps * (N + 1) * nreduce * 8
-  / t (SURVEY.md 8d aggregate: sum over GPUs of the shard-fold bytes), t = the
-  max over ranks.  Then, in the same run: RCCL allreduce on the same buffers,
-  BASELINE config 4 (nreduce = 1 Gi, RCCL) and config 5 (float min/max/prod,
+  kernel over the members' device heaps (osgpu_heap_create: one contiguous
+  virtual range per PE, mapped into every member; xGMI); PE services from an
+  intra-node shared-memory runtime (tests/support/pe_shm.c); a sampled
+  bit-exact parity check against the oracle is reported.  value = steps *
+  (N + 1) * nreduce * 8 / t (SURVEY.md 8d aggregate: sum over GPUs of the
+  shard-fold bytes), t = the max over ranks.  Then, in the same run: RCCL
+  allreduce on the same buffers (forced: FP sum within tolerance), BASELINE
+  config 4 (nreduce = 1 Gi: the exact team kernel over the heaps, and RCCL
+  beside it) and config 5 (float min/max/prod,
   128 Mi per PE, host-resident, H2D/D2H included), fcollect64 over the
   device heaps (xGMI), RCCL and host staging, and config 1's small call
   (1 Ki ints) with host barriers vs the fused one-launch path.  A watchdog prints the line

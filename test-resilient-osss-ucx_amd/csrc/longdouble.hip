@@ -202,51 +202,38 @@ struct LdTeam {
 
 // owner-computes form (team.hip): every PE's own fold order, P(P-1) soft
 // ops per element; P is a template parameter so the P inputs stay in
-// registers.  x87 add and mul are commutative bit for bit (same rounding of
-// the same exact value; nan_pick is symmetric, x87.hpp), so member 1's fold
-// x1+x0+x2+... equals member 0's x0+x1+x2+...: sum and prod compute it once
-// (P-2 fewer soft ops).  min/max select by position and are not shared.
+// registers.  sum / prod: x87.hpp team_fold_sum_prod (P-1 folds advanced
+// in rounds); min / max select by position and fold one member at a time.
 // VEC: 16-byte aligned arrays (the x86-64 layout), one dwordx4 per element.
 template <int OP, int P, bool VEC>
 __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
 {
-    constexpr bool kCommutes = OP == 0 || OP == 1;
     const size_t stride = (size_t) gridDim.x * blockDim.x;
     for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        X80 x[P];
+        X80 x[P], r[P];
 #pragma unroll
         for (int p = 0; p < P; p++)
             x[p] = VEC ? unpack(__builtin_nontemporal_load(
                              reinterpret_cast<const u64x2 *>(a.src[p]) + i))
                        : load(a.src[p] + 16 * i);
-        // sum / prod: every input unpacked once, the folds run on unpacked values
-        XU u[P];
+        if (OP == 0 || OP == 1) {
+            team_fold_sum_prod<OP, P>(x, r);
+        } else {
 #pragma unroll
-        for (int p = 0; p < P; p++) u[p] = unpack_u(x[p]);
-        X80 r0 = x[0];
-#pragma unroll
-        for (int q = 0; q < P; q++) {
-            X80 acc;
-            if (q == 1 && kCommutes) {
-                acc = r0;
-            } else if (OP == 0 || OP == 1) {
-                XU ua = u[q];
-#pragma unroll
-                for (int j = 0; j < P; j++)
-                    if (j != q) ua = OP == 0 ? add_u(ua, u[j]) : mul_u(ua, u[j]);
-                acc = pack_u(ua);
-                if (q == 0) r0 = acc;
-            } else {
-                acc = x[q];
+            for (int q = 0; q < P; q++) {
+                X80 acc = x[q];
 #pragma unroll
                 for (int j = 0; j < P; j++)
                     if (j != q) acc = apply<OP>(acc, x[j]);
-                if (q == 0) r0 = acc;
+                r[q] = acc;
             }
+        }
+#pragma unroll
+        for (int q = 0; q < P; q++) {
             if (VEC)
-                __builtin_nontemporal_store(pack(acc), reinterpret_cast<u64x2 *>(a.dst[q]) + i);
+                __builtin_nontemporal_store(pack(r[q]), reinterpret_cast<u64x2 *>(a.dst[q]) + i);
             else
-                store(a.dst[q] + 16 * i, acc);
+                store(a.dst[q] + 16 * i, r[q]);
         }
     }
 }

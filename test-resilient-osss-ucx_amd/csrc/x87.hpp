@@ -111,55 +111,54 @@ struct XU {
 OSGPU_HD inline XU unpack_u(X80 x) { return XU{x.m, x.se & kEmax, (x.se >> 15) & 1}; }
 OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s << 15) | x.e}; }
 
-// add of two NORMAL operands (0 < biased exponent < 0x7fff, J set) whose
-// exponents differ by less than 64 (or by 66 and more: the smaller is then
-// below the rounding bit and the RNE result is the larger) and whose result
-// stays normal -- what every soft-float add of ordinary data is: the same
-// exact-then-round computation as add_general, on 64-bit halves, with the
-// data-dependent choices (swap, add or subtract, carry or renormalise, round
-// up) made by selects so the lanes of a wave run one instruction stream.
-// false: not covered (gaps of 64 and 65, cancellation into the low half,
-// underflow) -- add_general takes it.  Bit-identical by construction (same
-// aligned operand, same rounding) and by test (tests/test_x87_softfloat.py
-// compiles this header for the host).
-OSGPU_HD inline bool add_normal(XU a, XU b, XU *r)
+OSGPU_HD inline bool normal_u(XU x) { return x.e - 1u < kEmax - 1u && (x.m >> 63); }
+
+// add of two NORMAL operands (0 < biased exponent < 0x7fff, J set; the
+// caller checks), straight-line: the data-dependent choices (swap, add or
+// subtract, renormalising shift, round up) are selects, so the lanes of a
+// wave -- and several independent folds of one lane -- run one instruction
+// stream.  Returns false where it does not apply: exponent gaps of 64 and 65,
+// cancellation into the low half (exact zero included), results below the
+// normal range or overflowing, a significand of all ones rounded up to the
+// next power of two; add_general then computes the result.
+//
+// Same exact-then-round computation as add_general, one bit lower: the
+// operands sit in 128 bits with one bit of headroom (A = ma * 2^63,
+// B = mb * 2^(63-d), exact for d < 64), so a carry lands in bit 127 instead
+// of leaving the word, and addition and subtraction share one normalising
+// left shift by clz (0 or 1 after an addition).  For d >= 66 B is dropped:
+// it lies below a quarter of A's ulp and RNE returns A.
+OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
 {
     const bool swap = b.e > a.e || (b.e == a.e && b.m > a.m);  // |A| >= |B|
-    const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
-    const int EA = (int) (swap ? b.e : a.e);
-    const int d = EA - (int) (swap ? a.e : b.e);
+    const uint64_t ma = swap ? b.m : a.m;
+    uint64_t mb = swap ? a.m : b.m;
+    const uint32_t EA = swap ? b.e : a.e;
+    const uint32_t d = EA - (swap ? a.e : b.e);
     const uint32_t sign = swap ? b.s : a.s;
-    if (d >= 66) {
-        *r = XU{ma, (uint32_t) EA, sign};
-        return true;
-    }
-    if (d >= 64) return false;
-    const bool same = a.s == b.s;
-    // B = mb * 2^-d as 64.64 fixed point, exact for d < 64
-    const uint64_t bh = mb >> d;
-    const uint64_t bl = d ? mb << ((64 - d) & 63) : 0;
-    const uint64_t hs = ma + bh;
-    const bool c = same && hs < ma;  // carry out of bit 127
-    uint64_t hi = same ? hs : ma - bh - (bl != 0 ? 1 : 0);
-    uint64_t lo = same ? bl : 0 - bl;
-    if (!same && hi == 0) return false;  // cancellation into the low half
-    // renormalise: right by one on a carry, left by lz after a subtraction
-    const int lz = same ? 0 : __builtin_clzll(hi);
-    const uint64_t hr = (hi >> 1) | (1ull << 63), lr = (lo >> 1) | (hi << 63) | (lo & 1);
-    const uint64_t hl = lz ? (hi << lz) | (lo >> ((64 - lz) & 63)) : hi, ll = lo << lz;
-    hi = c ? hr : hl;
-    lo = c ? lr : ll;
-    int E = EA + (c ? 1 : -lz);
-    if (E < 1) return false;  // gradual underflow
-    // round to nearest even at bit 64
-    const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
-    hi += up ? 1 : 0;
-    const bool wrap = up && hi == 0;  // carried out of 64 bits
-    hi = wrap ? (1ull << 63) : hi;
-    E += wrap ? 1 : 0;
-    const bool inf = E >= (int) kEmax;
-    *r = XU{inf ? (1ull << 63) : hi, inf ? kEmax : (uint32_t) E, sign};
-    return true;
+    mb = d >= 64 ? 0 : mb;
+    const unsigned sh = d & 63;  // d >= 64: mb == 0
+    const u128 A = ((u128) (ma >> 1) << 64) | (ma << 63);
+    const u128 B = ((u128) ((mb >> sh) >> 1) << 64) | (mb << (63 - sh));
+    // A + B, or A - B as ~(~A + B), without a data-dependent branch
+    const uint32_t m32 = 0u - (a.s ^ b.s);
+    const uint64_t M = ((uint64_t) m32 << 32) | m32;
+    const u128 MM = ((u128) M << 64) | M;
+    const u128 S = ((A ^ MM) + B) ^ MM;
+    uint64_t hi = (uint64_t) (S >> 64), lo = (uint64_t) S;
+    const bool cancel = hi == 0;
+    const int lz = __builtin_clzg(hi, 64);  // 64 only when cancel (flagged)
+    const unsigned l6 = lz & 63;
+    hi = (hi << l6) | ((lo >> 1) >> (63 - l6));
+    lo <<= l6;
+    int E = (int) EA + 1 - lz;
+    const bool low = E < 1;
+    // round to nearest even at bit 64: up when lo > 2^63, or lo == 2^63 and
+    // hi is odd
+    hi += lo > (1ull << 63) - (hi & 1) ? 1 : 0;
+    const bool wrap = hi == 0;  // carried out of 64 bits (all ones rounded up)
+    *r = XU{hi, (uint32_t) E, sign};
+    return d - 64u >= 2u && !cancel && !low && !wrap && E < (int) kEmax;
 }
 
 // The fast form when it applies, else the general add (out of line: a fold
@@ -169,9 +168,7 @@ OSGPU_HD inline bool add_normal(XU a, XU b, XU *r)
 OSGPU_HD inline XU add_u(XU a, XU b)
 {
     XU r;
-    if (a.e - 1u < kEmax - 1u && b.e - 1u < kEmax - 1u && ((a.m & b.m) >> 63) &&
-        add_normal(a, b, &r))
-        return r;
+    if (normal_u(a) && normal_u(b) && add_fast(a, b, &r)) return r;
     return unpack_u(add_general(pack_u(a), pack_u(b)));
 }
 
@@ -232,32 +229,34 @@ OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b)
 
 OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b);
 
-// mul of two NORMAL operands whose product stays normal: the exact 128-bit
-// product of two significands with J set lies in [2^126, 2^128), so the
-// renormalising shift is 0 or 1 (a select), then one RNE rounding at bit 64
-// -- the general path's computation without its classification and
-// variable shifts.  Everything else goes to mul_general.
+// mul of two NORMAL operands (the caller checks), straight-line: the exact
+// 128-bit product of two significands with J set lies in [2^126, 2^128), so
+// the renormalising shift is 0 or 1 (a select), then one RNE rounding at bit
+// 64 -- the general path's computation without its classification and
+// variable shifts.  false: the product leaves the normal range (denormal or
+// infinity) or its rounding carries out of the significand; mul_general
+// computes it.
+OSGPU_HD inline bool mul_fast(XU a, XU b, XU *r)
+{
+    const u128 P = (u128) a.m * (u128) b.m;
+    uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
+    const bool top = (hi >> 63) != 0;
+    const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
+    hi = top ? hi : h1;
+    lo = top ? lo : l1;
+    // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = S * 2^(E-bias-127)
+    int E = (int) a.e + (int) b.e - kBias + (top ? 1 : 0);
+    const bool low = E < 1;
+    hi += lo > (1ull << 63) - (hi & 1) ? 1 : 0;  // RNE at bit 64 (add_fast)
+    const bool wrap = hi == 0;
+    *r = XU{hi, (uint32_t) E, a.s ^ b.s};
+    return !low && !wrap && E < (int) kEmax;
+}
+
 OSGPU_HD inline XU mul_u(XU a, XU b)
 {
-    if (a.e - 1u < kEmax - 1u && b.e - 1u < kEmax - 1u && ((a.m & b.m) >> 63)) {
-        const u128 P = (u128) a.m * (u128) b.m;
-        uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
-        const bool top = (hi >> 63) != 0;
-        const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
-        hi = top ? hi : h1;
-        lo = top ? lo : l1;
-        // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = S * 2^(E-bias-127)
-        int E = (int) a.e + (int) b.e - kBias + (top ? 1 : 0);
-        if (E >= 1) {
-            const bool up = (lo >> 63) && ((lo << 1) != 0 || (hi & 1));
-            hi += up ? 1 : 0;
-            const bool wrap = up && hi == 0;
-            hi = wrap ? (1ull << 63) : hi;
-            E += wrap ? 1 : 0;
-            const bool inf = E >= (int) kEmax;
-            return XU{inf ? (1ull << 63) : hi, inf ? kEmax : (uint32_t) E, a.s ^ b.s};
-        }
-    }
+    XU r;
+    if (normal_u(a) && normal_u(b) && mul_fast(a, b, &r)) return r;
     return unpack_u(mul_general(pack_u(a), pack_u(b)));
 }
 
@@ -284,6 +283,72 @@ OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
     //   = S * 2^(E - bias - 127)  =>  E = Ea + Eb - bias + 1 - lz
     const int E = Ea + Eb - kBias + 1 - lz;
     return round_pack(s, E, P);
+}
+
+// Every member's fold of a P-PE sum (OP 0) or prod (OP 1) of one element,
+// each in its own order (src/reductions.c:79-111: PE q starts from its own
+// x_q, then x_0, x_1, ... skipping q).  x87 add and mul are commutative bit
+// for bit (same rounding of the same exact value; nan_pick is symmetric), so
+// member 1's fold x1 op x0 op x2 ... equals member 0's: P-1 folds, not P.
+//
+// The folds advance in rounds: round t applies every fold's t-th operand
+// with the straight-line fast op, so the P-1 independent chains interleave
+// in one instruction stream (ILP for a VALU-bound kernel); only when some
+// lane of the wave has an operand or result outside the fast op's range
+// does the round take the general op, for those folds and lanes.  A fold
+// whose running value leaves the normal range stays on the general op
+// (`slow`) until it is normal again.
+template <int OP, int P>
+OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
+{
+    constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
+    XU u[P];
+    bool nrm[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        u[p] = unpack_u(x[p]);
+        nrm[p] = normal_u(u[p]);
+    }
+    XU acc[NF];
+    bool slow[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        const int q = f == 0 ? 0 : f + 1;
+        acc[f] = u[q];
+        slow[f] = !nrm[q];
+    }
+#pragma unroll
+    for (int t = 0; t < P - 1; t++) {
+        XU res[NF];
+        bool ok[NF];
+        bool all = true;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            const int q = f == 0 ? 0 : f + 1;
+            const int j = t < q ? t : t + 1;  // q's t-th operand
+            const bool fast = OP == 0 ? add_fast(acc[f], u[j], &res[f])
+                                      : mul_fast(acc[f], u[j], &res[f]);
+            ok[f] = fast && !slow[f] && nrm[j];
+            all = all && ok[f];
+        }
+        if (!all) {
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                if (!ok[f]) {
+                    const int q = f == 0 ? 0 : f + 1;
+                    const int j = t < q ? t : t + 1;
+                    res[f] = unpack_u(OP == 0 ? add_general(pack_u(acc[f]), pack_u(u[j]))
+                                              : mul_general(pack_u(acc[f]), pack_u(u[j])));
+                    slow[f] = !normal_u(res[f]);
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; f++) acc[f] = res[f];
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++) out[f == 0 ? 0 : f + 1] = pack_u(acc[f]);
+    out[1] = out[0];
 }
 
 // fcomi ordering; false when unordered (NaN or unsupported encoding)

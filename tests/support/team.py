@@ -209,4 +209,6 @@ def build_x87check():
     L = ctypes.CDLL(X87_PATH)
     L.x87check_op.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_size_t]
+    L.x87check_team.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_size_t]
     return L

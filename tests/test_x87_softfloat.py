@@ -5,6 +5,7 @@ payloads, unnormals, pseudo-denormals, pseudo-infinities/NaNs, subnormals,
 extremes) and on random raw encodings across the whole exponent range.
 The same source runs on the MI355X in longdouble.hip (tests/test_gpu_parity.py).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -118,7 +119,7 @@ def _pairs(where, n=60_000):
 
 @pytest.mark.parametrize("where", ["unit", "underflow", "overflow"])
 def test_aligned_operand_boundaries(x87, where):
-    """The normal-operand fast path of x87 add (x87.hpp add_normal): exponent
+    """The normal-operand fast path of x87 add (x87.hpp add_fast): exponent
     differences around the 64-bit shift seams (0-3, 62-67, 70, 120, 200),
     significands next to powers of two (borrow / carry / renormalise cases),
     both signs, near 1, near the underflow threshold (results on the denormal
@@ -145,3 +146,40 @@ def test_equal_and_opposite_operands(x87):
     b = O.from_value_bytes("longdouble", neg.reshape(-1))
     check(x87, a, a, use_ref=O.ref_lib() is not None)
     check(x87, a, b, use_ref=O.ref_lib() is not None)
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("op", ["sum", "prod"])
+def test_team_fold_rounds(x87, op, P):
+    """The team kernel's fold of every member (x87.hpp team_fold_sum_prod:
+    P-1 folds advanced in rounds, fast op with a general fallback per round,
+    member 1 sharing member 0's fold) against the reference's per-PE fold
+    order (oracle to_all), on data that sends some lanes and rounds to the
+    general op: mostly normal values near 1 with cancellations, plus zeros,
+    denormals, infinities, NaNs and values near overflow."""
+    n = 40_000
+    srcs = []
+    for p in range(P):
+        x = raw_random(n, 100 + p, "near")
+        raw = O.value_bytes(x).reshape(-1, 10).copy()
+        k = O.splitmix64(300 + p, n)
+        for sel, mode in ((1, "any"), (2, "low"), (3, "high")):
+            idx = np.nonzero((k % np.uint64(53)) == np.uint64(sel))[0]
+            raw[idx] = O.value_bytes(raw_random(n, 500 + 7 * p + sel, mode)).reshape(-1, 10)[idx]
+        srcs.append(np.ascontiguousarray(O.from_value_bytes("longdouble", raw.reshape(-1))))
+    if op == "sum":             # exact cancellations against member 0's value
+        neg = O.value_bytes(srcs[0]).reshape(-1, 10).copy()
+        neg[:, 9] ^= 0x80
+        raw1 = O.value_bytes(srcs[1]).reshape(-1, 10).copy()
+        raw1[::17] = neg[::17]
+        srcs[1] = np.ascontiguousarray(O.from_value_bytes("longdouble", raw1.reshape(-1)))
+    want = O.to_all("longdouble", op, srcs)
+    got = [np.zeros_like(srcs[0]) for _ in range(P)]
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in srcs])
+    dp = (ctypes.c_void_p * P)(*[g.ctypes.data for g in got])
+    assert x87.x87check_team(0 if op == "sum" else 1, P, sp, dp, n) == 0
+    for q in range(P):
+        w = O.value_bytes(want[q]).reshape(-1, 10)
+        g = O.value_bytes(got[q]).reshape(-1, 10)
+        bad = np.nonzero((w != g).any(1))[0]
+        assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"
