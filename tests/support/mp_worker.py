@@ -38,6 +38,7 @@ import ctypes
 import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
@@ -651,6 +652,81 @@ def device_heap_modes(L, PES, mode, rank, world):
     return res
 
 
+def mixpush_mode(L, PES, rank, world, iters=24):
+    """Host-heap calls (STAGED path through the set's staging buffers)
+    alternating with device-heap calls on the push form of the team
+    exchange, which scatters into the same staging buffers: a PE that
+    leaves the staged call early must not overwrite slots a slower peer is
+    still draining into its host target (run_team_push barriers before its
+    first scatter).  Arrival order is jittered per call; every result is
+    compared bit for bit with the oracle."""
+    import random
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    H = 1 << 23
+    heap = torch.zeros(H, dtype=torch.uint8, device="cuda:0")
+    h = (ctypes.c_char * 64)()
+    assert L.osgpu_ipc_get_handle(ctypes.c_void_p(heap.data_ptr()), h) == 0
+    hs = [None] * world
+    dist.all_gather_object(hs, bytes(h))
+    mapped = []
+    for pe in range(world):
+        if pe == rank:
+            b = heap.data_ptr()
+        else:
+            b = L.osgpu_ipc_open((ctypes.c_char * 64).from_buffer_copy(hs[pe]))
+            assert b, L.osgpu_last_error().decode()
+            mapped.append(b)
+        assert L.osgpu_heap_register(pe, ctypes.c_void_p(b), H) == 0
+    base = PES.pes_heap(rank)
+    psync = base + (1 << 24) - 4096
+    nh, nd = 300_007, 200_003
+    hsrc = [O.gen_input("double", nh, O.pe_seed(0x51, r), "wide") for r in range(world)]
+    dsrc = [O.gen_input("double", nd, O.pe_seed(0x52, r), "wide") for r in range(world)]
+    want_h = O.value_bytes(O.to_all("double", "sum", hsrc)[rank]).reshape(-1).tobytes()
+    want_d = O.value_bytes(O.to_all("double", "sum", dsrc)[rank]).reshape(-1).tobytes()
+    raw_h = np.ascontiguousarray(hsrc[rank]).view(np.uint8).reshape(-1)
+    ctypes.memmove(base, raw_h.ctypes.data, raw_h.size)
+    htgt = base + (1 << 23)
+    heap[: nd * 8].copy_(torch.from_numpy(np.ascontiguousarray(dsrc[rank]).view(np.uint8).copy()))
+    dtoff = 4 << 20
+    torch.cuda.synchronize()
+    os.environ["OSGPU_HOST_PATH"] = "staged"
+    L.osgpu_set_fused_max_bytes(0)          # host barriers: the staged pipeline
+    rng = random.Random(rank * 7919 + 1)
+    bad = {"host": 0, "device": 0}
+    paths = set()
+    wrk = (ctypes.c_byte * 4096)()
+    dist.barrier()
+    for it in range(iters):
+        ctypes.memset(htgt, 0, nh * 8)
+        time.sleep(rng.random() * 0.004)
+        L.osgpu_set_team_exchange(0)
+        L.shmem_double_sum_to_all(htgt, base, nh, 0, 0, world, wrk, psync)
+        paths.add(osgpu.last_path())
+        if ctypes.string_at(htgt, nh * 8) != want_h:
+            bad["host"] += 1
+        time.sleep(rng.random() * 0.004)
+        L.osgpu_set_team_exchange(1)
+        L.shmem_double_sum_to_all(heap.data_ptr() + dtoff, heap.data_ptr(), nd, 0, 0, world,
+                                  wrk, psync)
+        paths.add(osgpu.last_path())
+        torch.cuda.synchronize()
+        if heap[dtoff:dtoff + nd * 8].cpu().numpy().tobytes() != want_d:
+            bad["device"] += 1
+        heap[dtoff:dtoff + nd * 8].zero_()
+        torch.cuda.synchronize()
+    L.osgpu_set_team_exchange(-1)
+    L.osgpu_set_fused_max_bytes(-1)
+    os.environ.pop("OSGPU_HOST_PATH", None)
+    dist.barrier()
+    L.osgpu_finalize()
+    for p in mapped:
+        L.osgpu_ipc_close(ctypes.c_void_p(p))
+    return {"mixpush_bad": bad, "mixpush_paths": sorted(paths)}
+
+
 def main():
     mode, outdir = sys.argv[1], sys.argv[2]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -660,7 +736,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm", "late"):
+            "timeout", "vmm", "late", "mixpush"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -713,6 +789,8 @@ def main():
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
         os.environ.pop("OSGPU_HOST_PATH", None)
         res["out"] = out
+    if mode == "mixpush":
+        res.update(mixpush_mode(L, PES, rank, world))
     if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout", "late"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "vmm":

@@ -140,6 +140,23 @@ def test_ipc_heaps_two_processes(tmp_path, monkeypatch, pes):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
+def test_staged_then_push_processes(tmp_path, world, monkeypatch):
+    """A host-heap call (STAGED, 64 KiB chunks) followed by a device-heap call
+    on the push form of the team exchange, 24 times with jittered arrivals:
+    both scatter through the set's staging buffers, and every result stays
+    bit-exact (the push exchange barriers before its first scatter)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("OSGPU_STAGE_BYTES", "65536")
+    res = launch("mixpush", world, tmp_path)
+    for r in res:
+        assert r["mixpush_bad"] == {"host": 0, "device": 0}, r
+        assert r["mixpush_paths"] == ["staged", "team_push"], r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
 def test_host_staged_processes(tmp_path, world, monkeypatch):
     """Host symmetric heaps (shared memory), one process per PE -- the
     reference's own data placement.  STAGED: H2D -> exchange through the
