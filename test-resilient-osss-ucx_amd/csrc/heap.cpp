@@ -164,8 +164,16 @@ bool recv_fds(int s, std::vector<int> &fds)
         do r = recvmsg(s, &msg, MSG_CMSG_CLOEXEC); while (r < 0 && errno == EINTR);
         if (r != 1) return false;
         cmsghdr *cm = CMSG_FIRSTHDR(&msg);
-        if (!cm || cm->cmsg_type != SCM_RIGHTS) return false;
+        if (!cm || cm->cmsg_type != SCM_RIGHTS || (msg.msg_flags & MSG_CTRUNC)) return false;
         const int got = (int) ((cm->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+        if (got <= 0 || got > m) {      // a batch carries 1..m descriptors
+            if (got > 0) {
+                int tmp[kFdBatch];
+                memcpy(tmp, CMSG_DATA(cm), sizeof(int) * std::min(got, kFdBatch));
+                for (int k = 0; k < std::min(got, kFdBatch); k++) close(tmp[k]);
+            }
+            return false;
+        }
         const size_t at = fds.size();
         fds.resize(at + got);
         memcpy(fds.data() + at, CMSG_DATA(cm), sizeof(int) * got);
