@@ -203,7 +203,8 @@ struct LdTeam {
 // owner-computes form (team.hip): every PE's own fold order, P(P-1) soft
 // ops per element; P is a template parameter so the P inputs stay in
 // registers.  sum / prod: x87.hpp team_fold_sum_prod (P-1 folds advanced
-// in rounds); min / max select by position and fold one member at a time.
+// in rounds); max / min: team_fold_minmax (P key compares, then every
+// member's pick among the tied extremes).
 // VEC: 16-byte aligned arrays (the x86-64 layout), one dwordx4 per element.
 template <int OP, int P, bool VEC>
 __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
@@ -218,15 +219,11 @@ __global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
                        : load(a.src[p] + 16 * i);
         if (OP == 0 || OP == 1) {
             team_fold_sum_prod<OP, P>(x, r);
-        } else {
-#pragma unroll
-            for (int q = 0; q < P; q++) {
-                X80 acc = x[q];
-#pragma unroll
-                for (int j = 0; j < P; j++)
-                    if (j != q) acc = apply<OP>(acc, x[j]);
-                r[q] = acc;
-            }
+        } else if (P > 2) {
+            team_fold_minmax<OP, P>(x, r);
+        } else {  // two members: one compare each
+            r[0] = apply<OP>(x[0], x[1]);
+            r[1] = apply<OP>(x[1], x[0]);
         }
 #pragma unroll
         for (int q = 0; q < P; q++) {

@@ -41,6 +41,17 @@ struct TeamPtrs {
 
 constexpr int kTeamBlock = 256;
 
+// above 4 members: U vectors per input per lane, G of them in flight per
+// round.  U = G = 2 (16 vectors of 16 B in flight per lane at 8 members, one
+// round) beat U = 4 in two rounds of 2 by 1-3 % at P = 8, every type
+// (profiles/r02_team_variants.jsonl); the pull combine keeps OSGPU_U_K8
+#ifndef OSGPU_TEAM_U8
+#define OSGPU_TEAM_U8 2
+#endif
+#ifndef OSGPU_TEAM_G8
+#define OSGPU_TEAM_G8 OSGPU_TEAM_U8
+#endif
+
 template <typename T, int OP, int P, bool ORDERED>
 __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
 {
@@ -68,7 +79,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                                                               int nedge)
 {
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
+    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_TEAM_U8);
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -98,9 +109,9 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
     if (t0 + (size_t) (U - 1) * kTeamBlock < nvec) {
         // whole tile: the loads of G vectors of every input are in flight
         // before the first fold, as in combine_vec_kernel -- P*G*16 B per
-        // lane, not P*16 B per round trip.  G = U up to 4 inputs; above, two
-        // rounds of U/2 (all U*P at once spills the 8-input complex sum)
-        constexpr int G = P <= 4 ? U : (U > 1 ? U / 2 : 1);
+        // lane, not P*16 B per round trip.  G = U up to 4 inputs; above,
+        // OSGPU_TEAM_G8 (all 4*P at once spills the 8-input complex sum)
+        constexpr int G = P <= 4 ? U : OSGPU_TEAM_G8;
 #pragma unroll
         for (int g = 0; g < U; g += G) {
             TVec<T> in[G][P];
@@ -119,13 +130,14 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const size_t j = t0 + (size_t) u * kTeamBlock;
-        if (j >= nvec) break;
-        TVec<T> in[P];
+        if (j < nvec) {
+            TVec<T> in[P];
 #pragma unroll
-        for (int p = 0; p < P; p++)
-            in[p].v = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4 *>(a.src[p] + head) + j);
-        fold_store(in, j);
+            for (int p = 0; p < P; p++)
+                in[p].v = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4 *>(a.src[p] + head) + j);
+            fold_store(in, j);
+        }
     }
 }
 
@@ -166,7 +178,7 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
+    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_TEAM_U8);
     size_t head = phase ? (16 - phase) / sizeof(T) : 0;
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;

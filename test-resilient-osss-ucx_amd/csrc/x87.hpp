@@ -351,6 +351,76 @@ OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
     out[1] = out[0];
 }
 
+OSGPU_HD inline bool less(X80 a, X80 b);
+
+// Every member's fold of a P-PE max (OP 5) or min (OP 6) of one element.
+// The fold acc = (acc < b ? acc : b) (min; > for max, miscops.c:80-105)
+// visits x_q, then x_0, x_1, ... skipping q, and keeps the LAST visited
+// element with the extreme value (a tie hands over to the incoming b).  So
+// with t1 = the highest index holding the extreme and t2 the next highest,
+// member q gets x_t1 unless q == t1, which gets x_t2 (x_t1 if alone) -- the
+// same encodings the P(P-1) compares select, from P compares.  Values are
+// ordered by a 16+64-bit key (positive: 0x8000|e : m; negative:
+// 0x7fff-e : ~m; zeros as +0), which is fcomi's order on zeros, denormals,
+// normals and infinities.  Any NaN or unsupported / pseudo-denormal encoding
+// in the element sends it to the compare-by-compare folds.
+template <int OP, int P>
+OSGPU_HD inline void team_fold_minmax(const X80 (&x)[P], X80 (&out)[P])
+{
+    uint32_t kh[P];
+    uint64_t kl[P];
+    bool ord = true;
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        const uint32_t e = x[p].se & kEmax;
+        const uint64_t m = x[p].m;
+        const bool J = (m >> 63) != 0;
+        ord = ord && (e == 0 ? !J : (e == kEmax ? m == (1ull << 63) : J));
+        const bool neg = ((x[p].se >> 15) & 1) && (e | m) != 0;
+        kh[p] = neg ? kEmax - e : 0x8000u | e;
+        kl[p] = neg ? ~m : m;
+    }
+    if (!ord) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            X80 acc = x[q];
+#pragma unroll
+            for (int j = 0; j < P; j++)
+                if (j != q) acc = (OP == 5 ? less(x[j], acc) : less(acc, x[j])) ? acc : x[j];
+            out[q] = acc;
+        }
+        return;
+    }
+    uint32_t bh = kh[0];
+    uint64_t bl = kl[0];
+#pragma unroll
+    for (int p = 1; p < P; p++) {
+        const bool lt = kh[p] < bh || (kh[p] == bh && kl[p] < bl);
+        const bool gt = kh[p] > bh || (kh[p] == bh && kl[p] > bl);
+        const bool take = OP == 5 ? gt : lt;
+        bh = take ? kh[p] : bh;
+        bl = take ? kl[p] : bl;
+    }
+    int t1 = -1, t2 = -1;  // the highest and next highest index holding it
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        const bool eq = kh[p] == bh && kl[p] == bl;
+        t2 = eq ? t1 : t2;
+        t1 = eq ? p : t1;
+    }
+    X80 v1 = x[0], v2 = x[0];
+    const int s2 = t2 >= 0 ? t2 : t1;
+#pragma unroll
+    for (int p = 1; p < P; p++) {
+        v1.m = p == t1 ? x[p].m : v1.m;
+        v1.se = p == t1 ? x[p].se : v1.se;
+        v2.m = p == s2 ? x[p].m : v2.m;
+        v2.se = p == s2 ? x[p].se : v2.se;
+    }
+#pragma unroll
+    for (int q = 0; q < P; q++) out[q] = q == t1 ? v2 : v1;
+}
+
 // fcomi ordering; false when unordered (NaN or unsupported encoding)
 OSGPU_HD inline bool less(X80 a, X80 b)
 {

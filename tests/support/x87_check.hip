@@ -37,8 +37,8 @@ extern "C" int x87check_op(int op, const void *a, const void *b, void *out, size
     return 0;
 }
 
-// every member's result of a P-PE sum / prod, as the team kernel folds them
-// (x87.hpp team_fold_sum_prod): srcs[p] and dsts[p] are arrays of n 16-B
+// every member's result of a P-PE sum / prod / max / min, as the team kernel
+// folds them (x87.hpp team_fold_sum_prod, team_fold_minmax): srcs[p] and dsts[p] are arrays of n 16-B
 // elements
 template <int OP, int P>
 static void team_p(const unsigned char *const *srcs, unsigned char *const *dsts, size_t n)
@@ -46,7 +46,10 @@ static void team_p(const unsigned char *const *srcs, unsigned char *const *dsts,
     for (size_t i = 0; i < n; i++) {
         X80 x[P], r[P];
         for (int p = 0; p < P; p++) x[p] = ld(srcs[p] + 16 * i);
-        team_fold_sum_prod<OP, P>(x, r);
+        if (OP == 0 || OP == 1)
+            team_fold_sum_prod<OP, P>(x, r);
+        else
+            team_fold_minmax<OP, P>(x, r);
         for (int p = 0; p < P; p++) {
             unsigned char *o = dsts[p] + 16 * i;
             __builtin_memset(o, 0, 16);
@@ -64,9 +67,11 @@ extern "C" int x87check_team(int op, int P, const void *const *srcs, void *const
 #define TP(PP)                                                                 \
     case PP:                                                                   \
         if (op == 0) team_p<0, PP>(S, D, n);                                   \
-        else team_p<1, PP>(S, D, n);                                           \
+        else if (op == 1) team_p<1, PP>(S, D, n);                              \
+        else if (op == 5) team_p<5, PP>(S, D, n);                              \
+        else team_p<6, PP>(S, D, n);                                           \
         return 0;
-    if (op != 0 && op != 1) return -1;
+    if (op != 0 && op != 1 && op != 5 && op != 6) return -1;
     switch (P) { TP(2) TP(3) TP(4) TP(5) TP(6) TP(7) TP(8) }
 #undef TP
     return -1;

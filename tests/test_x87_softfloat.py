@@ -183,3 +183,49 @@ def test_team_fold_rounds(x87, op, P):
         g = O.value_bytes(got[q]).reshape(-1, 10)
         bad = np.nonzero((w != g).any(1))[0]
         assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("op", ["max", "min"])
+def test_team_fold_minmax(x87, op, P):
+    """The team kernel's max / min (x87.hpp team_fold_minmax: one key scan,
+    then each member's pick among tied extremes) against the reference's
+    per-PE fold order: values from a small pool so that extremes tie across
+    PEs -- +0 against -0, equal denormals, infinities, duplicated normals --
+    with NaNs, pseudo-denormals and unsupported encodings in some elements
+    (the compare-by-compare fold)."""
+    n = 60_000
+    pool = np.zeros((12, 10), np.uint8)
+
+    def enc(m, e, sgn):
+        b = np.zeros(10, np.uint8)
+        b[:8] = np.frombuffer(np.uint64(m).tobytes(), np.uint8)
+        b[8:10] = np.frombuffer(np.uint16(e | (sgn << 15)).tobytes(), np.uint8)
+        return b
+    vals = [(0, 0, 0), (0, 0, 1), (1 << 40, 0, 0), (1 << 40, 0, 1), (1 << 63, 0x7FFF, 0),
+            (1 << 63, 0x7FFF, 1), (0xC000000000000000, 0x3FFF, 0), (0xC000000000000000, 0x3FFF, 1),
+            (1 << 63, 1, 0), (1 << 63, 1, 1), (0x8000000000000001, 0x7FFE, 0),
+            (0x8000000000000001, 0x7FFE, 1)]
+    for i, v in enumerate(vals):
+        pool[i] = enc(*v)
+    specials = O.value_bytes(raw_random(n, 900, "any")).reshape(-1, 10)
+    srcs = []
+    for p in range(P):
+        k = O.splitmix64(700 + p, n)
+        raw = pool[(k % np.uint64(12)).astype(np.int64)].copy()
+        # a narrower pool in some elements makes ties likely at every P
+        narrow = (k >> np.uint64(8)) % np.uint64(3) == 0
+        raw[narrow] = pool[((k[narrow] >> np.uint64(16)) % np.uint64(2)).astype(np.int64)]
+        sp = (k >> np.uint64(24)) % np.uint64(29) == 0
+        raw[sp] = specials[sp]
+        srcs.append(np.ascontiguousarray(O.from_value_bytes("longdouble", raw.reshape(-1))))
+    want = O.to_all("longdouble", op, srcs)
+    got = [np.zeros_like(srcs[0]) for _ in range(P)]
+    sptr = (ctypes.c_void_p * P)(*[s.ctypes.data for s in srcs])
+    dptr = (ctypes.c_void_p * P)(*[g.ctypes.data for g in got])
+    assert x87.x87check_team(5 if op == "max" else 6, P, sptr, dptr, n) == 0
+    for q in range(P):
+        w = O.value_bytes(want[q]).reshape(-1, 10)
+        g = O.value_bytes(got[q]).reshape(-1, 10)
+        bad = np.nonzero((w != g).any(1))[0]
+        assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"

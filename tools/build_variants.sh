@@ -2,19 +2,22 @@
 # Build libosgpu_reduce variants with different per-lane unroll depths
 # (OSGPU_U_K2/K4/K8) into tools/variants/ for tools/variant_sweep.py.
 #   VARIANTS="421 442 444" tools/build_variants.sh   (digits: U for K<=2, K<=4, K<=8)
+#   a fourth digit sets OSGPU_TEAM_G8 (team kernel, vectors in flight per
+#   input above 4 PEs), e.g. "4482"
 set -e
 cd "$(dirname "$0")/../test-resilient-osss-ucx_amd/csrc"
 make -s -j8
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math"
 TAGS=${VARIANTS:-"421 442 422 441 842"}
 for t in $TAGS; do
-  a=${t:0:1}; b=${t:1:1}; c=${t:2:1}
+  a=${t:0:1}; b=${t:1:1}; c=${t:2:1}; g=${t:3:1}
   d=../../tools/variants/u$t; mkdir -p $d
-  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$a -DOSGPU_U_K4=$b -DOSGPU_U_K8=$c -c combine.hip -o $d/combine.o &
-  /opt/rocm/bin/hipcc $FL -DOSGPU_U_K2=$a -DOSGPU_U_K4=$b -DOSGPU_U_K8=$c -c team.hip -o $d/team.o &
+  X="-DOSGPU_U_K2=$a -DOSGPU_U_K4=$b -DOSGPU_U_K8=$c ${g:+-DOSGPU_TEAM_G8=$g}"
+  /opt/rocm/bin/hipcc $FL $X -c combine.hip -o $d/combine.o &
+  /opt/rocm/bin/hipcc $FL $X -c team.hip -o $d/team.o &
 done
 wait
-OTHERS="fused.o verify.o longdouble.o copy.o runtime.o shmem_reduce.o shmem_collect.o"
+OTHERS="fused.o verify.o longdouble.o copy.o runtime.o heap.o shmem_reduce.o shmem_collect.o"
 for t in $TAGS; do
   d=../../tools/variants/u$t
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
