@@ -386,7 +386,12 @@ OSGPU_HD inline void team_fold_minmax(const X80 (&x)[P], X80 (&out)[P])
             X80 acc = x[q];
 #pragma unroll
             for (int j = 0; j < P; j++)
-                if (j != q) acc = (OP == 5 ? less(x[j], acc) : less(acc, x[j])) ? acc : x[j];
+                if (j != q) {  // field by field: a select of whole structs
+                               // makes the compiler address x through scratch
+                    const bool keep = OP == 5 ? less(x[j], acc) : less(acc, x[j]);
+                    acc.m = keep ? acc.m : x[j].m;
+                    acc.se = keep ? acc.se : x[j].se;
+                }
             out[q] = acc;
         }
         return;
@@ -401,24 +406,28 @@ OSGPU_HD inline void team_fold_minmax(const X80 (&x)[P], X80 (&out)[P])
         bh = take ? kh[p] : bh;
         bl = take ? kl[p] : bl;
     }
-    int t1 = -1, t2 = -1;  // the highest and next highest index holding it
+    // the highest index holding it (t1, value v1) and the value at the next
+    // highest (v2; v1 when t1 is alone), carried along the scan
+    int t1 = -1;
+    bool two = false;
+    X80 v1 = x[0], v2 = x[0];
 #pragma unroll
     for (int p = 0; p < P; p++) {
         const bool eq = kh[p] == bh && kl[p] == bl;
-        t2 = eq ? t1 : t2;
+        v2.m = eq && t1 >= 0 ? v1.m : v2.m;
+        v2.se = eq && t1 >= 0 ? v1.se : v2.se;
+        two = two || (eq && t1 >= 0);
+        v1.m = eq ? x[p].m : v1.m;
+        v1.se = eq ? x[p].se : v1.se;
         t1 = eq ? p : t1;
     }
-    X80 v1 = x[0], v2 = x[0];
-    const int s2 = t2 >= 0 ? t2 : t1;
+    v2.m = two ? v2.m : v1.m;
+    v2.se = two ? v2.se : v1.se;
 #pragma unroll
-    for (int p = 1; p < P; p++) {
-        v1.m = p == t1 ? x[p].m : v1.m;
-        v1.se = p == t1 ? x[p].se : v1.se;
-        v2.m = p == s2 ? x[p].m : v2.m;
-        v2.se = p == s2 ? x[p].se : v2.se;
+    for (int q = 0; q < P; q++) {  // member q: v1 unless q == t1
+        out[q].m = q == t1 ? v2.m : v1.m;
+        out[q].se = q == t1 ? v2.se : v1.se;
     }
-#pragma unroll
-    for (int q = 0; q < P; q++) out[q] = q == t1 ? v2 : v1;
 }
 
 // fcomi ordering; false when unordered (NaN or unsupported encoding)
