@@ -140,11 +140,13 @@ OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
     const unsigned sh = d & 63;  // d >= 64: mb == 0
     const u128 A = ((u128) (ma >> 1) << 64) | (ma << 63);
     const u128 B = ((u128) ((mb >> sh) >> 1) << 64) | (mb << (63 - sh));
-    // A + B, or A - B as ~(~A + B), without a data-dependent branch
-    const uint32_t m32 = 0u - (a.s ^ b.s);
+    // A + B, or A - B as A + ~B + 1, without a data-dependent branch (the
+    // + 1 rides in as the carry into the low word, whose A half is zero)
+    const uint32_t diff = a.s ^ b.s;
+    const uint32_t m32 = 0u - diff;
     const uint64_t M = ((uint64_t) m32 << 32) | m32;
     const u128 MM = ((u128) M << 64) | M;
-    const u128 S = ((A ^ MM) + B) ^ MM;
+    const u128 S = A + (B ^ MM) + (u128) diff;
     uint64_t hi = (uint64_t) (S >> 64), lo = (uint64_t) S;
     const bool cancel = hi == 0;
     const int lz = __builtin_clzg(hi, 64);  // 64 only when cancel (flagged)
