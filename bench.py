@@ -752,6 +752,12 @@ def bench_multi(args):
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     ndev = torch.cuda.device_count()
+    if 0 < ndev < world:
+        # ranks sharing a GPU (a rehearsal): at most 16 hardware queues on
+        # it between them, or its scheduler time-slices them in milliseconds
+        # (INTEGRATION.md); set before the first HIP call of this process
+        per_gpu = -(-world // ndev)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(1, 16 // per_gpu)))
     dev_id = local % max(ndev, 1)
     torch.cuda.set_device(dev_id)
     dev = torch.device("cuda", dev_id)

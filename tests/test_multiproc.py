@@ -39,9 +39,18 @@ def launch(mode, world, tmp_path, timeout=600):
     logdir = os.environ.get("MP_LOG_DIR") or str(tmp_path)
     os.makedirs(logdir, exist_ok=True)
     procs = []
+    extra = {}
+    # PE processes sharing one GPU: at most 16 hardware queues between them
+    # (HIP's default is four per process; more than 16 on the GPU and its
+    # scheduler time-slices the queues in milliseconds, INTEGRATION.md,
+    # profiles/r02_mp_latency_hwq.jsonl).  MP_HWQ=default keeps HIP's default.
+    if world > 4 and "GPU_MAX_HW_QUEUES" not in os.environ and \
+            os.environ.get("MP_HWQ") != "default":
+        extra["GPU_MAX_HW_QUEUES"] = str(max(1, 16 // world))
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1",
+                   **extra)
         log = os.path.join(logdir, f"{mode}_w{world}_rank{r}.log")
         f = open(log, "w")
         procs.append((subprocess.Popen([sys.executable, WORKER, mode, str(tmp_path)], env=env,
