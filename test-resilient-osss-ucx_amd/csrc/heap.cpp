@@ -325,6 +325,15 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     H->own.device = dev;
     H->own.bytes = total;
     H->own.len = chunk_lens(total, chunk);
+    {  // more than the device has free cannot succeed: fail at once instead
+       // of creating chunks until the HBM runs out
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && total > fr) {
+            set_err("%s: %zu B requested, %zu B free on device %d", where, total, fr, dev);
+            ok = false;
+        }
+        (void) hipGetLastError();
+    }
     for (size_t k = 0; ok && k < H->own.len.size(); k++) {
         hipMemGenericAllocationHandle_t h;
         if (hipMemCreate(&h, H->own.len[k], &prop, 0) != hipSuccess) {

@@ -548,7 +548,7 @@ long pci_key(int dev)
 // barriers); every member returns the same verdict.  pSync is returned zeroed.
 bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &peer,
                  std::vector<void *> &opened, int *ndev, bool distinct_processes,
-                 int *max_share)
+                 int *max_share, int *procs_here)
 {
     int dev = 0;
     HIPCHK(c.name, hipGetDevice(&dev));
@@ -565,6 +565,7 @@ bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &
     bool ok = local != nullptr;
     peer.assign(c.PE_size, nullptr);
     std::vector<long> pcis(1, mine->pci), all_pci(1, mine->pci);
+    std::vector<long> pids_here(1, mine->pid);  // processes on my GPU
     for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
         if (pe == c.me) {
             peer[i] = local;
@@ -574,6 +575,9 @@ bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &
         c.ops.getmem(&m, mine, sizeof(m), pe);
         all_pci.push_back(m.pci);
         if (std::find(pcis.begin(), pcis.end(), m.pci) == pcis.end()) pcis.push_back(m.pci);
+        if (m.pci == mine->pci &&
+            std::find(pids_here.begin(), pids_here.end(), m.pid) == pids_here.end())
+            pids_here.push_back(m.pid);
         if (m.slot != (long) bytes) {
             ok = false;
         } else if (m.pid == (long) getpid()) {
@@ -604,6 +608,7 @@ bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &
     barrier(c);
     memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
     if (ndev) *ndev = (int) pcis.size();
+    if (procs_here) *procs_here = (int) pids_here.size();
     if (max_share) {
         int mx = 0;
         for (long k : pcis) mx = std::max(mx, (int) std::count(all_pci.begin(), all_pci.end(), k));
@@ -645,13 +650,25 @@ StageSet *stage_setup(const Coll &c)
     S.device = dev;
     S.slot = stage_slot_bytes();
     HIPCHK(c.name, hipMalloc((void **) &S.local, 4 * S.slot));
-    device_copy_streams(c.name, dev, &S.st_in, &S.st_out);
-    HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_c, hipStreamNonBlocking));
     for (int s = 0; s < 2; s++) {
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_in[s], hipEventDisableTiming));
         HIPCHK(c.name, hipEventCreateWithFlags(&S.ev_out[s], hipEventDisableTiming));
     }
-    S.ok = map_members(c, S.local, S.slot, S.peer, S.opened, &S.ndev, false, nullptr);
+    int procs_here = 1;
+    S.ok = map_members(c, S.local, S.slot, S.peer, S.opened, &S.ndev, false, nullptr,
+                       &procs_here);
+    if (procs_here > 1) {
+        // PE processes sharing this GPU also share its hardware queue slots
+        // (HIP gives each process up to 4; past 16 on the GPU its scheduler
+        // time-slices them in milliseconds) and its PCIe link:
+        // the staging copies and folds go on the PE's own stream, in order,
+        // so this process holds no queue beyond it
+        S.st_in = S.st_out = S.st_c = pe_ctx(c.name, c.me).stream;
+    } else {
+        device_copy_streams(c.name, dev, &S.st_in, &S.st_out);
+        HIPCHK(c.name, hipStreamCreateWithFlags(&S.st_c, hipStreamNonBlocking));
+        S.own_c = true;
+    }
     return S.ok ? &S : nullptr;
 }
 
@@ -1036,7 +1053,7 @@ int osgpu_finalize(void)
             if (S.ev_in[s]) (void) hipEventDestroy(S.ev_in[s]);
             if (S.ev_out[s]) (void) hipEventDestroy(S.ev_out[s]);
         }
-        if (S.st_c) (void) hipStreamDestroy(S.st_c);
+        if (S.st_c && S.own_c) (void) hipStreamDestroy(S.st_c);
     }
     g_stage.clear();
     for (auto &kv : g_copy_streams) {  // shared by the staging sets above

@@ -150,6 +150,7 @@ struct StageSet {
     std::vector<char *> peer;        // by active-set index
     std::vector<void *> opened;      // IPC mappings to close
     hipStream_t st_in = nullptr, st_c = nullptr, st_out = nullptr;
+    bool own_c = false;              // st_c created for this set (else the PE's stream)
     hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
     char *in(int i, int s) const { return peer[i] + (size_t) s * slot; }
     char *out(int i, int s) const { return peer[i] + (size_t) (2 + s) * slot; }
@@ -160,10 +161,11 @@ StageSet *stage_setup(const Coll &c);
 // Publish a device allocation to every member of the active set and map
 // every member's (collective; the same verdict on every member).
 // distinct_processes: fail unless every member is its own process.
-// max_share: the largest number of members on one GPU.
+// max_share: the largest number of members on one GPU.  procs_here: the
+// processes among the members on this process's GPU (this one included).
 bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &peer,
                  std::vector<void *> &opened, int *ndev, bool distinct_processes,
-                 int *max_share);
+                 int *max_share, int *procs_here = nullptr);
 
 // ------------------------------------------------- device-side barriers
 
