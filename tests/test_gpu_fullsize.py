@@ -1,0 +1,107 @@
+"""BASELINE configs 4 and 5 at their full sizes on one MI355X, through the
+kernel shmem_<T>_<op>_to_all dispatches for a P-PE call (the owner-computes
+team kernel, osgpu_team_combine in the C ABI: one launch does every member's
+shard, as the P PEs' launches do together on P GPUs).
+
+Every member's target is checked bit for bit against the reference's fold
+order for that member (src/reductions.c:79-111: PE q starts from its own
+source, then PE 0, 1, ... skipping q), restated with PyTorch element-wise
+IEEE operations in that order (no contraction: one rounding per operation,
+the reference's SSE arithmetic for float/double).
+
+* config 4: double sum, nreduce = 1 Gi (8 GiB per array), 8 PEs
+  (64 GiB of sources, 64 GiB of targets);
+* config 5: float min / max / prod, nreduce = 128 Mi (512 MiB per array),
+  8 PEs -- the device-resident part of that config (its H2D/D2H staging is
+  tests/test_gpu_parity.py and test_multiproc.py).
+"""
+import ctypes
+
+import pytest
+
+import osgpu
+
+pytestmark = pytest.mark.gpu
+
+P = 8
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _team(torch, t, op, srcs, dsts, n):
+    L = osgpu.load()
+    S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs])
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts])
+    # the inputs were written on torch's stream; a NULL stream would be the
+    # library's non-blocking one, which does not wait for them
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream().cuda_stream
+    rc = L.osgpu_team_combine(osgpu.TYPES.index(t), osgpu.OPS.index(op), P, D, S, n,
+                              ctypes.c_void_p(st))
+    assert rc == 0, L.osgpu_last_error().decode()
+    torch.cuda.synchronize()
+
+
+def _fold(torch, op, srcs, q):
+    """Member q's result in its own order (reductions.c:84-111)."""
+    f = {"sum": torch.add, "prod": torch.mul,
+         # a<b?a:b / a>b?a:b with a the accumulator (miscops.c:80-105)
+         "min": lambda a, b: torch.where(a < b, a, b),
+         "max": lambda a, b: torch.where(a > b, a, b)}[op]
+    acc = srcs[q].clone()
+    for j in range(P):
+        if j != q:
+            acc = f(acc, srcs[j])
+    return acc
+
+
+def _need(torch, nbytes):
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    if free < nbytes:
+        pytest.skip(f"needs {nbytes >> 30} GiB of free HBM, {free >> 30} GiB free")
+
+
+def test_config4_double_sum_1Gi_8_pes(torch_cuda):
+    torch = torch_cuda
+    n = 1 << 30
+    _need(torch, (2 * P + 2) * n * 8)
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    srcs = [torch.empty(n, dtype=torch.float64, device="cuda:0").uniform_(1.0, 2.0, generator=g)
+            for _ in range(P)]
+    dsts = [torch.empty(n, dtype=torch.float64, device="cuda:0") for _ in range(P)]
+    _team(torch, "double", "sum", srcs, dsts, n)
+    for q in range(P):
+        want = _fold(torch, "sum", srcs, q)
+        assert torch.equal(dsts[q].view(torch.int64), want.view(torch.int64)), q
+        del want
+    # every member's fold starts from its own source: with 8 addends in
+    # [1, 2) the orders round differently, so targets differ between members
+    assert not torch.equal(dsts[0], dsts[7])
+    del srcs, dsts
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("op,lo,hi", [("min", -1e3, 1e3), ("max", -1e3, 1e3),
+                                      ("prod", 0.9, 1.1)])
+def test_config5_float_128Mi_8_pes(torch_cuda, op, lo, hi):
+    torch = torch_cuda
+    n = 128 << 20
+    _need(torch, (2 * P + 2) * n * 4)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    srcs = [torch.empty(n, dtype=torch.float32, device="cuda:0").uniform_(lo, hi, generator=g)
+            for _ in range(P)]
+    dsts = [torch.empty(n, dtype=torch.float32, device="cuda:0") for _ in range(P)]
+    _team(torch, "float", op, srcs, dsts, n)
+    for q in range(P):
+        want = _fold(torch, op, srcs, q)
+        assert torch.equal(dsts[q].view(torch.int32), want.view(torch.int32)), (op, q)
+        del want
+    del srcs, dsts
+    torch.cuda.empty_cache()
