@@ -192,28 +192,17 @@ hipMemAllocationProp chunk_prop(int dev)
     return p;
 }
 
-// read-write access from this process's current device (required); for the
-// PE's own heap (`own`) also from every other visible device that can reach
-// it as a peer -- PEs that are threads of this process on other GPUs use
-// the range directly (best effort)
-bool grant_access(char *base, size_t bytes, int dev, bool own)
+// read-write access to a mapped range from device `dev`
+bool grant_access(char *base, size_t bytes, int dev)
 {
     hipMemAccessDesc d;
     memset(&d, 0, sizeof(d));
     d.location.type = hipMemLocationTypeDevice;
     d.location.id = dev;
     d.flags = hipMemAccessFlagsProtReadWrite;
-    if (hipMemSetAccess(base, bytes, &d, 1) != hipSuccess) return false;
-    int ndev = 0;
-    if (!own || hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
-    for (int o = 0; o < ndev; o++) {
-        int can = 0;
-        if (o == dev || hipDeviceCanAccessPeer(&can, o, dev) != hipSuccess || !can) continue;
-        d.location.id = o;
-        if (hipMemSetAccess(base, bytes, &d, 1) != hipSuccess) (void) hipGetLastError();
-    }
+    const bool ok = hipMemSetAccess(base, bytes, &d, 1) == hipSuccess;
     (void) hipGetLastError();
-    return true;
+    return ok;
 }
 
 void unmap(Mapping &m)
@@ -236,8 +225,9 @@ std::vector<size_t> chunk_lens(size_t bytes, size_t chunk)
     return v;
 }
 
-// reserve one range and map `h` (lengths `len`) back to back into it
-bool map_chunks(Mapping &m, size_t align, int dev, bool own)
+// reserve one range and map `h` (lengths `len`) back to back into it,
+// readable and writable from this process's device
+bool map_chunks(Mapping &m, size_t align, int dev)
 {
     void *va = nullptr;
     if (hipMemAddressReserve(&va, m.bytes, align, nullptr, 0) != hipSuccess) return false;
@@ -247,7 +237,7 @@ bool map_chunks(Mapping &m, size_t align, int dev, bool own)
         if (hipMemMap(m.base + off, m.len[k], 0, m.h[k], 0) != hipSuccess) return false;
         m.nmapped = k + 1;
     }
-    return grant_access(m.base, m.bytes, dev, own);
+    return grant_access(m.base, m.bytes, dev);
 }
 
 size_t heap_chunk_bytes(size_t gran)
@@ -354,7 +344,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     }
     DBG("%s PE %d: %zu chunks of %zu B created and exported (ok=%d)", where, c.me,
         H->own.len.size(), chunk, (int) ok);
-    if (ok && !map_chunks(H->own, gran, dev, true)) {
+    if (ok && !map_chunks(H->own, gran, dev)) {
         set_err("%s: mapping the heap failed", where);
         ok = false;
     }
@@ -398,6 +388,17 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         if (msg[i].bytes <= 0) ok = false;
     }
     for (int i = 0; i < PE_size; i++) H->seg = std::max(H->seg, (int) msg[i].seg);
+    // members that are threads of this process on another GPU use my range
+    // directly: their devices need access to it too (only theirs -- a grant
+    // binds this process to that GPU, which one-process-per-GPU jobs never
+    // need); done before the status barrier below, after which they use it
+    for (int i = 0; ok && i < PE_size; i++) {
+        if (c.pe_at(i) == c.me || msg[i].pid != (long) getpid() || msg[i].device == dev) continue;
+        if (!grant_access(H->own.base, H->own.bytes, (int) msg[i].device)) {
+            set_err("%s: device %ld cannot access PE %d's heap", where, msg[i].device, c.me);
+            ok = false;
+        }
+    }
     int expected = 0;
     for (int i = 0; i < PE_size; i++)
         if (c.pe_at(i) != c.me && msg[i].pid != (long) getpid()) expected++;
@@ -484,7 +485,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             (void) write_all(s, &ack, 1);
             close(s);
         }
-        if (got && !map_chunks(m, gran, dev, false)) {
+        if (got && !map_chunks(m, gran, dev)) {
             set_err("%s: mapping PE %d's heap failed", where, pe);
             got = false;
         }
