@@ -205,13 +205,24 @@ bool grant_access(char *base, size_t bytes, int dev)
     return ok;
 }
 
+// Unmap and release a heap's chunks.  The virtual range of a heap imported
+// from another process stays reserved: on this ROCm (7.2) a range that held
+// imported chunks and is freed and reserved again -- for a later heap of
+// this process or a later import -- keeps reaching the OLD chunks from the
+// GPU (every unmap / release / free call succeeds; reductions in the new
+// heap read and write the old memory: test_heap_create_destroy_cycles_
+// processes), so such a range is never handed back (address space only).
 void unmap(Mapping &m)
 {
     size_t off = 0;
+    int bad = 0;
     for (size_t k = 0; k < m.nmapped; off += m.len[k], k++)
-        (void) hipMemUnmap(m.base + off, m.len[k]);
-    for (auto h : m.h) (void) hipMemRelease(h);
-    if (m.base) (void) hipMemAddressFree(m.base, m.bytes);
+        bad += hipMemUnmap(m.base + off, m.len[k]) != hipSuccess;
+    for (auto h : m.h) bad += hipMemRelease(h) != hipSuccess;
+    const bool imported = m.pe >= 0 && m.device < 0;
+    if (m.base && !imported) bad += hipMemAddressFree(m.base, m.bytes) != hipSuccess;
+    DBG("heap unmap: PE %d's range %p (%zu B, %zu chunks): %d failed calls", m.pe,
+        (void *) m.base, m.bytes, m.h.size(), bad);
     (void) hipGetLastError();
     m = Mapping();
 }

@@ -92,6 +92,71 @@ def run_colls(L, rank, world, src_addr, tgt_addr, psync, out, tag, write, read):
         dist.barrier()
 
 
+def heap_cycle_mode(L, PES, rank, world, cycles=6):
+    """osgpu_heap_create / osgpu_heap_destroy repeated with growing sizes,
+    and two heaps alive at once: each heap gets its own registry segment,
+    a reduction inside each is bit-exact, destroying frees the HBM (free
+    memory returns to its starting level) and unregisters the ranges."""
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    wrk = (ctypes.c_byte * 4096)()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    segs, bad = [], 0
+    for k in range(cycles):
+        bases = []
+        for h in range(2):                     # two heaps alive at once
+            nbytes = (64 << 20) * (k + 1) + (h << 21)
+            bp = ctypes.c_void_p()
+            rc = L.osgpu_heap_create(nbytes, 0, 0, world, psync, ctypes.byref(bp))
+            assert rc == 0, (rc, L.osgpu_last_error().decode())
+            bases.append((bp.value, nbytes))
+        for base, nbytes in bases:
+            n = min(nbytes // 16, 1 << 20)
+            src = O.gen_input("double", n, O.pe_seed(0xC0 + k, rank), "wide")
+            raw = np.ascontiguousarray(src).view(np.uint8)
+            stage = torch.from_numpy(raw.copy()).cuda()
+            torch.cuda.synchronize()   # osgpu.copy's default stream does not wait for torch's
+            osgpu.copy([base], [stage.data_ptr()], [raw.size])
+            torch.cuda.synchronize()
+            PES.pes_barrier(0, 0, world, None)
+            L.shmem_double_sum_to_all(base + nbytes // 2, base, n, 0, 0, world, wrk, psync)
+            got = np.empty(n * 8, np.uint8)
+            torch.cuda.synchronize()
+            got_t = torch.empty(n * 8, dtype=torch.uint8, device="cuda:0")
+            osgpu.copy([got_t.data_ptr()], [base + nbytes // 2], [n * 8])
+            torch.cuda.synchronize()
+            got[:] = got_t.cpu().numpy()
+            allsrc = [O.gen_input("double", n, O.pe_seed(0xC0 + k, r), "wide")
+                      for r in range(world)]
+            want = O.value_bytes(O.to_all("double", "sum", allsrc)[rank]).reshape(-1)
+            ok_ = bool(np.array_equal(got, want))
+            bad += int(not ok_)
+            if not ok_:
+                diff = np.nonzero(got != want)[0]
+                print(f"heapcycle rank {rank} cycle {k} heap {bases.index((base, nbytes))}: "
+                      f"{diff.size} bytes differ, first {diff[:4].tolist()}, base {base:#x}, "
+                      f"path {osgpu.last_path()}", flush=True)
+            segs.append(int(L.osgpu_heap_translate(base, rank, rank) == base))
+            PES.pes_barrier(0, 0, world, None)
+        print(f"heapcycle rank {rank} cycle {k}: bases {[hex(b_) for b_, _ in bases]} "
+              f"free {torch.cuda.mem_get_info()[0] >> 20} MiB", flush=True)
+        for base, _ in bases:
+            assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
+            # the range is no longer a registered heap
+            assert L.osgpu_heap_translate(base, rank, rank) in (0, None)
+        PES.pes_barrier(0, 0, world, None)
+        print(f"heapcycle rank {rank} cycle {k} destroyed: free "
+              f"{torch.cuda.mem_get_info()[0] >> 20} MiB", flush=True)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    return {"heap_cycles": cycles, "heap_cycle_bad": bad, "heap_translated": segs,
+            "free_drop_MiB": (free0 - free1) / 2**20}
+
+
 def vmm_heap_mode(L, PES, rank, world):
     """osgpu_heap_create: one contiguous device heap per PE (virtual-memory
     chunks exported as dmabuf descriptors), every member's mapped here.
@@ -736,7 +801,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm", "late", "mixpush"):
+            "timeout", "vmm", "late", "mixpush", "heapcycle"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -795,6 +860,8 @@ def main():
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "vmm":
         res.update(vmm_heap_mode(L, PES, rank, world))
+    if mode == "heapcycle":
+        res.update(heap_cycle_mode(L, PES, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096
         buf = PES.pes_heap(rank)

@@ -326,6 +326,27 @@ def test_fused_collectives_processes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_heap_create_destroy_cycles_processes(tmp_path):
+    """osgpu_heap_create / osgpu_heap_destroy six times over, two heaps
+    alive at once, 2 processes: every reduction inside every heap bit-exact
+    (a new heap's range must not reach an old heap's memory: heap.cpp keeps
+    imported ranges reserved), ranges registered while alive and
+    unregistered after destroy.  The HBM of heaps that another process
+    imported does not come back before the processes exit on this ROCm
+    (every unmap / release call succeeds): the drop is
+    recorded and bounded by the bytes of all heaps made."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("heapcycle", 2, tmp_path, timeout=300)
+    made_MiB = 2 * sum(2 * 64 * (k + 1) + 2 for k in range(6))   # both processes
+    for r in res:
+        assert r["heap_cycle_bad"] == 0, r
+        assert all(r["heap_translated"]), r
+        assert r["free_drop_MiB"] < made_MiB + 512, r
+
+
+@pytest.mark.gpu
 def test_vmm_heap_large_objects_processes(tmp_path):
     """osgpu_heap_create with three processes on cuda:0: each PE's device heap
     is ONE contiguous virtual range of dmabuf-exported chunks, mapped whole
