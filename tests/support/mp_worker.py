@@ -92,6 +92,64 @@ def run_colls(L, rank, world, src_addr, tgt_addr, psync, out, tag, write, read):
         dist.barrier()
 
 
+def finalize_cycle_mode(L, PES, rank, world, cycles=4):
+    """osgpu_finalize between rounds of calls, 2 processes: every round
+    re-creates the staging sets, the device-barrier flag areas and their
+    HIP IPC mappings (the previous ones closed), then runs a host-staged
+    reduce, a fused small device call and a team device call on an
+    osgpu_heap_create heap -- each checked bit for bit."""
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    hsync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 4096
+    bp = ctypes.c_void_p()
+    assert L.osgpu_heap_create(64 << 20, 0, 0, world, hsync, ctypes.byref(bp)) == 0
+    base = bp.value
+    hbase = PES.pes_heap(rank)
+    wrk = (ctypes.c_byte * 4096)()
+    bad = []
+    paths = set()
+    for k in range(cycles):
+        for what, n, dev in (("staged", 300_007, False), ("fused", 1000, True),
+                             ("team", 1 << 20, True)):
+            srcs = [O.gen_input("double", n, O.pe_seed(0xF0 + 3 * k + len(what), r), "wide")
+                    for r in range(world)]
+            want = O.value_bytes(O.to_all("double", "sum", srcs)[rank]).reshape(-1)
+            raw = np.ascontiguousarray(srcs[rank]).view(np.uint8).reshape(-1)
+            if dev:
+                stage = torch.from_numpy(raw.copy()).cuda()
+                torch.cuda.synchronize()
+                osgpu.copy([base], [stage.data_ptr()], [raw.size])
+                torch.cuda.synchronize()
+                src, tgt = base, base + (32 << 20)
+            else:
+                ctypes.memmove(hbase, raw.ctypes.data, raw.size)
+                src, tgt = hbase, hbase + (4 << 20)
+                os.environ["OSGPU_HOST_PATH"] = "staged"
+            PES.pes_barrier(0, 0, world, None)
+            L.shmem_double_sum_to_all(tgt, src, n, 0, 0, world, wrk, psync)
+            ran = osgpu.last_path()
+            os.environ.pop("OSGPU_HOST_PATH", None)
+            if dev:
+                out_t = torch.empty(n * 8, dtype=torch.uint8, device="cuda:0")
+                osgpu.copy([out_t.data_ptr()], [tgt], [n * 8])
+                torch.cuda.synchronize()
+                got = out_t.cpu().numpy()
+            else:
+                got = np.frombuffer(ctypes.string_at(tgt, n * 8), np.uint8)
+            if not np.array_equal(got, want):
+                bad.append((k, what, ran))
+            paths.add(ran)
+            PES.pes_barrier(0, 0, world, None)
+        assert L.osgpu_finalize() == 0
+        PES.pes_barrier(0, 0, world, None)
+    PES.pes_barrier(0, 0, world, None)
+    assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
+    return {"finalize_cycles": cycles, "finalize_bad": bad, "finalize_paths": sorted(paths)}
+
+
 def heap_cycle_mode(L, PES, rank, world, cycles=6):
     """osgpu_heap_create / osgpu_heap_destroy repeated with growing sizes,
     and two heaps alive at once: each heap gets its own registry segment,
@@ -801,7 +859,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm", "late", "mixpush", "heapcycle"):
+            "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -862,6 +920,8 @@ def main():
         res.update(vmm_heap_mode(L, PES, rank, world))
     if mode == "heapcycle":
         res.update(heap_cycle_mode(L, PES, rank, world))
+    if mode == "finalizecycle":
+        res.update(finalize_cycle_mode(L, PES, rank, world))
     if mode == "hostcoll":
         psync = PES.pes_heap(rank) + (1 << 24) - 4096
         buf = PES.pes_heap(rank)

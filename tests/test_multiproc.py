@@ -326,6 +326,20 @@ def test_fused_collectives_processes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_finalize_cycles_processes(tmp_path):
+    """osgpu_finalize between rounds, 2 processes: the staging sets, flag
+    areas and their IPC mappings are made again each round, and a
+    host-staged reduce, a fused small call and a team call stay bit-exact."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("finalizecycle", 2, tmp_path, timeout=300)
+    for r in res:
+        assert r["finalize_bad"] == [], r
+        assert r["finalize_paths"] == ["fused_team", "staged", "team"], r
+
+
+@pytest.mark.gpu
 def test_heap_create_destroy_cycles_processes(tmp_path):
     """osgpu_heap_create / osgpu_heap_destroy six times over, two heaps
     alive at once, 2 processes: every reduction inside every heap bit-exact
