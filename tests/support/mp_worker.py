@@ -150,6 +150,32 @@ def finalize_cycle_mode(L, PES, rank, world, cycles=4):
     return {"finalize_cycles": cycles, "finalize_bad": bad, "finalize_paths": sorted(paths)}
 
 
+def heap_leak_mode(L, PES, rank, world):
+    """(probe, not a test) create / destroy heaps of MP_LEAK_GIB GiB per PE
+    MP_LEAK_CYCLES times: if destroyed heaps kept their HBM, the creates
+    would fail once the cycles add up to more than the GPU holds."""
+    import torch
+    torch.cuda.set_device(0)
+    PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    gib = int(os.environ.get("MP_LEAK_GIB", "16"))
+    cycles = int(os.environ.get("MP_LEAK_CYCLES", "20"))
+    done = 0
+    for k in range(cycles):
+        bp = ctypes.c_void_p()
+        rc = L.osgpu_heap_create(gib << 30, 0, 0, world, psync, ctypes.byref(bp))
+        if rc != 0:
+            return {"leak_cycles_done": done, "leak_fail": L.osgpu_last_error().decode(),
+                    "leak_gib": gib}
+        PES.pes_barrier(0, 0, world, None)
+        assert L.osgpu_heap_destroy(ctypes.c_void_p(bp.value)) == 0
+        PES.pes_barrier(0, 0, world, None)
+        done += 1
+        print(f"heapleak rank {rank} cycle {k} ok, free {torch.cuda.mem_get_info()[0] >> 30} GiB",
+              flush=True)
+    return {"leak_cycles_done": done, "leak_fail": None, "leak_gib": gib}
+
+
 def heap_cycle_mode(L, PES, rank, world, cycles=6):
     """osgpu_heap_create / osgpu_heap_destroy repeated with growing sizes,
     and two heaps alive at once: each heap gets its own registry segment,
@@ -859,7 +885,7 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle"):
+            "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle", "heapleak"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -920,6 +946,8 @@ def main():
         res.update(vmm_heap_mode(L, PES, rank, world))
     if mode == "heapcycle":
         res.update(heap_cycle_mode(L, PES, rank, world))
+    if mode == "heapleak":
+        res.update(heap_leak_mode(L, PES, rank, world))
     if mode == "finalizecycle":
         res.update(finalize_cycle_mode(L, PES, rank, world))
     if mode == "hostcoll":
