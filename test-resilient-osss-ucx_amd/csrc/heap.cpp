@@ -67,13 +67,21 @@ struct Mapping {                     // one heap as mapped in this process
 struct Heap {                        // the heap a PE created, with its imports
     int pe = -1;
     int seg = 0;                     // registry segment of every member's heap
+    long key = 0;                    // the same on every member: identifies this creation
     std::vector<int> members;
+    std::vector<char *> member_base; // every member's range as seen here, by set index
+    std::vector<size_t> member_bytes;
     Mapping own;
     std::vector<Mapping> peers;      // members in other processes
 };
 
 std::mutex g_hmu;
 std::vector<Heap *> g_heaps;
+// Destroyed heaps that hold chunks imported from other processes: their HBM
+// is not returned before the process exits on this ROCm, so
+// they are kept, fully mapped, and handed back when the same member set
+// creates a heap of the same size again (every member agrees on it).
+std::vector<Heap *> g_pool;
 
 // what a PE publishes in pSync[16..] during osgpu_heap_create
 struct HeapMsg {
@@ -321,6 +329,52 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     }
     const size_t total = (bytes + gran - 1) / gran * gran;
     const size_t chunk = std::min(heap_chunk_bytes(gran), total);
+    for (int i = 0; i < PE_size; i++) H->members.push_back(c.pe_at(i));
+
+    // a kept heap of this member set and size, if every member has one from
+    // the same creation: register it again instead of making a new one
+    HeapMsg *mine = reinterpret_cast<HeapMsg *>(pSync + kHeapPsync);
+    Heap *cand = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_hmu);
+        for (Heap *k : g_pool)
+            if (k->members == H->members && k->own.bytes == total && k->own.device == dev) {
+                cand = k;
+                break;
+            }
+    }
+    memset(mine, 0, sizeof(*mine));
+    mine->nonce = cand ? cand->key : 0;
+    mine->seg = heap_free_segment(H->members);
+    barrier(c);
+    bool reuse = cand != nullptr;
+    int rseg = (int) mine->seg;
+    for (int i = 0; i < PE_size; i++) {
+        const int pe = c.pe_at(i);
+        if (pe == c.me) continue;
+        HeapMsg m;
+        c.ops.getmem(&m, mine, sizeof(HeapMsg), pe);
+        reuse = reuse && m.nonce == mine->nonce;
+        rseg = std::max(rseg, (int) m.seg);
+    }
+    barrier(c);  // every member has read every message of this phase
+    memset(mine, 0, sizeof(*mine));
+    if (reuse) {
+        {
+            std::lock_guard<std::mutex> lk(g_hmu);
+            g_pool.erase(std::find(g_pool.begin(), g_pool.end(), cand));
+            cand->seg = rseg;
+            g_heaps.push_back(cand);
+        }
+        for (int i = 0; i < PE_size; i++)
+            osgpu_heap_register_segment(c.pe_at(i), rseg, cand->member_base[i],
+                                        cand->member_bytes[i]);
+        delete H;
+        *base_out = cand->own.base;
+        DBG("%s PE %d: kept heap %p of %zu B registered again (segment %d)", where, c.me,
+            (void *) cand->own.base, total, rseg);
+        return OSGPU_OK;
+    }
     std::vector<int> fds;
     H->own.pe = c.me;
     H->own.device = dev;
@@ -374,7 +428,6 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             ok = false;
         }
     }
-    HeapMsg *mine = reinterpret_cast<HeapMsg *>(pSync + kHeapPsync);
     memset(mine, 0, sizeof(*mine));
     mine->pid = (long) getpid();
     mine->nonce = nonce;
@@ -382,7 +435,6 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     mine->chunk = (long) chunk;
     mine->raw_ptr = (long) (uintptr_t) H->own.base;
     mine->device = dev;
-    for (int i = 0; i < PE_size; i++) H->members.push_back(c.pe_at(i));
     // every heap of a member set gets its own registry segment: the lowest
     // one free for every member here, agreed as the maximum over members
     mine->seg = heap_free_segment(H->members);
@@ -539,8 +591,15 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         if (ok) set_err("%s: another member failed to create or map its heap", where);
         return OSGPU_EPEER;
     }
-    for (int i = 0; i < PE_size; i++)
+    unsigned long long key = 0x9e3779b97f4a7c15ull;  // the same on every member
+    for (int i = 0; i < PE_size; i++) {
         osgpu_heap_register_segment(c.pe_at(i), H->seg, base[i], (size_t) msg[i].bytes);
+        H->member_base.push_back(base[i]);
+        H->member_bytes.push_back((size_t) msg[i].bytes);
+        key = (key ^ (unsigned long long) msg[i].pid) * 0x100000001b3ull;
+        key = (key ^ (unsigned long long) msg[i].nonce) * 0x100000001b3ull;
+    }
+    H->key = (long) (key | 1);  // never 0 (0 = "no kept heap")
     {
         std::lock_guard<std::mutex> lk(g_hmu);
         g_heaps.push_back(H);
@@ -570,7 +629,11 @@ extern "C" int osgpu_heap_destroy(void *base)
     (void) hipDeviceSynchronize();
     // forget the registrations that point into these ranges
     for (int pe : H->members) heap_clear_segment(pe, H->seg);
-    for (Mapping &m : H->peers) unmap(m);
+    if (!H->peers.empty()) {  // holds imported chunks: kept for a later heap
+        std::lock_guard<std::mutex> lk(g_hmu);
+        g_pool.push_back(H);
+        return OSGPU_OK;
+    }
     unmap(H->own);
     delete H;
     return OSGPU_OK;

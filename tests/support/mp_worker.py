@@ -158,22 +158,43 @@ def heap_leak_mode(L, PES, rank, world):
     torch.cuda.set_device(0)
     PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    import oracle as O
     gib = int(os.environ.get("MP_LEAK_GIB", "16"))
     cycles = int(os.environ.get("MP_LEAK_CYCLES", "20"))
-    done = 0
+    wrk = (ctypes.c_byte * 4096)()
+    rsync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 4096
+    done, bases, bad = 0, [], 0
     for k in range(cycles):
         bp = ctypes.c_void_p()
         rc = L.osgpu_heap_create(gib << 30, 0, 0, world, psync, ctypes.byref(bp))
         if rc != 0:
             return {"leak_cycles_done": done, "leak_fail": L.osgpu_last_error().decode(),
-                    "leak_gib": gib}
+                    "leak_gib": gib, "leak_bases": bases, "leak_bad": bad}
+        base = bp.value
+        bases.append(hex(base))
+        # a reduction at the far end of the heap
+        n = 1 << 20
+        off = (gib << 30) - 2 * n * 8
+        srcs = [O.gen_input("double", n, O.pe_seed(0x1EA + k, r), "wide") for r in range(world)]
+        want = O.value_bytes(O.to_all("double", "sum", srcs)[rank]).reshape(-1)
+        stage = torch.from_numpy(np.ascontiguousarray(srcs[rank]).view(np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        osgpu.copy([base + off], [stage.data_ptr()], [n * 8])
+        torch.cuda.synchronize()
         PES.pes_barrier(0, 0, world, None)
-        assert L.osgpu_heap_destroy(ctypes.c_void_p(bp.value)) == 0
+        L.shmem_double_sum_to_all(base + off + n * 8, base + off, n, 0, 0, world, wrk, rsync)
+        out_t = torch.empty(n * 8, dtype=torch.uint8, device="cuda:0")
+        osgpu.copy([out_t.data_ptr()], [base + off + n * 8], [n * 8])
+        torch.cuda.synchronize()
+        bad += int(not np.array_equal(out_t.cpu().numpy(), want))
+        PES.pes_barrier(0, 0, world, None)
+        assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
         PES.pes_barrier(0, 0, world, None)
         done += 1
         print(f"heapleak rank {rank} cycle {k} ok, free {torch.cuda.mem_get_info()[0] >> 30} GiB",
               flush=True)
-    return {"leak_cycles_done": done, "leak_fail": None, "leak_gib": gib}
+    return {"leak_cycles_done": done, "leak_fail": None, "leak_gib": gib, "leak_bases": bases,
+            "leak_bad": bad}
 
 
 def heap_cycle_mode(L, PES, rank, world, cycles=6):

@@ -340,6 +340,27 @@ def test_finalize_cycles_processes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_heap_reuse_processes(tmp_path, monkeypatch):
+    """Twelve rounds of a 32 GiB heap made and destroyed by 2 processes:
+    768 GiB in all, which the GPU only holds because a destroyed heap with
+    imported chunks is kept and handed back to the next create of the same
+    member set and size (heap.cpp g_pool) -- same base every round, and a
+    reduction at the heap's far end bit-exact each time."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if torch.cuda.mem_get_info()[1] < (100 << 30):
+        pytest.skip("needs a GPU of at least 100 GiB")
+    monkeypatch.setenv("MP_LEAK_GIB", "32")
+    monkeypatch.setenv("MP_LEAK_CYCLES", "12")
+    res = launch("heapleak", 2, tmp_path, timeout=400)
+    for r in res:
+        assert r["leak_fail"] is None and r["leak_cycles_done"] == 12, r
+        assert r["leak_bad"] == 0, r
+        assert len(set(r["leak_bases"])) == 1, r
+
+
+@pytest.mark.gpu
 def test_heap_create_destroy_cycles_processes(tmp_path):
     """osgpu_heap_create / osgpu_heap_destroy six times over, two heaps
     alive at once, 2 processes: every reduction inside every heap bit-exact
