@@ -249,9 +249,24 @@ def api_call_time(n, reps=20):
     return out
 
 
+def span_per_launch(torch, st, launch, reps):
+    """reps launches back to back on stream st, one HIP event pair around
+    them all: the average launch duration, kernel boundaries included (an
+    event pair around every launch would add its own gap to each)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(st)
+    for _ in range(reps):
+        launch()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e-3 / reps
+
+
 def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
-    """Median HIP-event time of osgpu_combine(K = 2) on its own stream over
-    n elements of two resident inputs; (K + 1) * n * esz bytes per launch."""
+    """Average launch time of osgpu_combine(K = 2) on its own stream over n
+    elements of two resident inputs (HIP event span over reps launches back
+    to back / reps); (K + 1) * n * esz bytes per launch."""
     dev = torch.device("cuda:0")
     a = torch.empty(n, dtype=dtype, device=dev)
     b = torch.empty(n, dtype=dtype, device=dev)
@@ -262,17 +277,12 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
     srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
     sp = ctypes.c_void_p(st.cuda_stream)
     torch.cuda.synchronize()
-    for _ in range(3):
+
+    def launch():
         assert L.osgpu_combine(type_code, op_code, out.data_ptr(), srcs, 2, n, sp) == 0
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(reps)]
-    for e0, e1 in ev:
-        e0.record(st)
-        L.osgpu_combine(type_code, op_code, out.data_ptr(), srcs, 2, n, sp)
-        e1.record(st)
-    torch.cuda.synchronize()
-    ts = sorted(e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev)
-    return ts[len(ts) // 2], a, b, out
+    for _ in range(3):
+        launch()
+    return span_per_launch(torch, st, launch, reps), a, b, out
 
 
 def team_kernel_rate(L, torch, n, reps):
@@ -299,9 +309,9 @@ def team_kernel_rate(L, torch, n, reps):
 
     for _ in range(3):
         launch()
+    kavg = span_per_launch(torch, st, launch, reps)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps)]
-    torch.cuda.synchronize()
     for e0, e1 in ev:
         e0.record(st)
         launch()
@@ -310,13 +320,14 @@ def team_kernel_rate(L, torch, n, reps):
     ks = [e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev]
     exact = bool(torch.equal(o0, a + b) and torch.equal(o1, b + a))
     B = 4 * n * 8
-    kavg = sum(ks) / len(ks)
     tr = load_traffic("team_vec_kernel<double, 0, 2, true>", n)
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
            "traffic": tr.get("bytes_per_launch") if tr else None,
            "kernel": "osgpu::team_vec_kernel<double, SUM, 2, ordered>",
-           "kernel_avg_us": kavg * 1e6, "kernel_min_us": min(ks) * 1e6,
+           "kernel_avg_us": kavg * 1e6,
+           "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
+           "kernel_min_us_per_launch_events": min(ks) * 1e6,
            "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact": exact,
            "note": "one launch over all nreduce elements = both PEs' shard launches of a 2-PE "
                    "call; 2 reads + 2 writes of 8 B per element"}
@@ -338,17 +349,12 @@ def stream_ceiling(L, torch, nbytes, reps=20):
     S = (ctypes.c_void_p * 1)(a.data_ptr())
     N = (ctypes.c_size_t * 1)(nbytes)
     torch.cuda.synchronize()
-    for _ in range(3):
+
+    def launch():
         assert L.osgpu_copy(D, S, N, 1, sp) == 0
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(reps)]
-    for e0, e1 in ev:
-        e0.record(st)
-        L.osgpu_copy(D, S, N, 1, sp)
-        e1.record(st)
-    torch.cuda.synchronize()
-    ts = sorted(e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev)
-    med = ts[len(ts) // 2]
+    for _ in range(3):
+        launch()
+    med = span_per_launch(torch, st, launch, reps)
     del a, o
     torch.cuda.empty_cache()
     return {"kernel": "copy_vec_kernel", "bytes_copied": nbytes, "us": med * 1e6,
@@ -444,18 +450,29 @@ def bench_single(args):
     idx = torch.randint(0, n, (4096,), device=dev)
     assert torch.equal(out[idx], a[idx] + b[idx])
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # timed region: the K launches back to back, one HIP event pair on the
+    # launch stream around all of them (an event pair around EVERY launch
+    # adds ≈ 6-8 µs per 255 µs launch, tools/warm_probe.py `gap`), so the
+    # average launch duration = event span / K, kernel boundaries included
+    e_beg, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
+    e_beg.record(stream)
+    for _ in range(args.steps):
         step()
-        ev[i][1].record(stream)
+    e_end.record(stream)
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
-    kms = [s.elapsed_time(e) for s, e in ev]
-    kavg = sum(kms) / len(kms) * 1e-3
+    kavg = e_beg.elapsed_time(e_end) * 1e-3 / args.steps
+    # after the timed region: the per-launch spread (an event pair per launch)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    kms = sorted(s.elapsed_time(e) for s, e in ev)
     B = 3 * n * 8
     res = {
         "metric": METRIC,
@@ -489,7 +506,9 @@ def bench_single(args):
         "traffic": tr.get("bytes_per_launch") if tr else None,
         "kernel": "osgpu::combine_vec_kernel<double, SUM, 2>",
         "kernel_avg_us": kavg * 1e6,
-        "kernel_min_us": min(kms) * 1e3,
+        "kernel_avg_how": "HIP event span over the K timed launches on the launch stream / K",
+        "kernel_median_us_per_launch_events": kms[len(kms) // 2] * 1e3,
+        "kernel_min_us_per_launch_events": kms[0] * 1e3,
         "algorithmic_bytes_per_launch": B,
     }
     # the kernel the API dispatches (TEAM path), under the same roofline
