@@ -107,11 +107,22 @@ def cpu_baseline(n):
     sec = O.cpu_baseline("double", "sum", src, reps=reps, pin=True)
     wall = time.time() - t0
     B = 2 * 3 * n * 8  # two PE results, each (K+1)*n*8
-    return {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
-            "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
-                       f"2 PEs (pthreads pinned to cores 0-1), nreduce={n}, median of "
-                       f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
-                       f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
+    out = {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
+           "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
+                      f"2 PEs (pthreads pinned to cores 0-1), nreduce={n}, median of "
+                      f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
+                      f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
+    # the same loop with every PE's elements split over 8 threads: 16 cores,
+    # this box's CPU share (a one-PE-per-core reference uses 2 for 2 PEs)
+    tpp = 8
+    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True, threads_per_pe=tpp)
+    reps16 = max(3, min(200, int(5.0 / max(probe, 1e-3))))
+    sec16 = O.cpu_baseline("double", "sum", src, reps=reps16, pin=True, threads_per_pe=tpp)
+    out["same_loop_16_cores"] = {
+        "value": B / sec16 / GIB, "unit": "GiB/s", "cores": 2 * tpp, "ms_per_call": sec16 * 1e3,
+        "sample": f"the same loop shape, each PE's elements split over {tpp} pinned threads "
+                  f"(cores 0-{2 * tpp - 1}), median of {reps16} after 1 warm-up"}
+    return out
 
 
 def cpu_baselines_configs():

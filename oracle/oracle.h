@@ -73,6 +73,12 @@ int oracle_to_all(int type, int op, int npes, int PE_start, int logPE_stride,
 double oracle_cpu_baseline(int type, int op, int npes,
                            const void *const *sources, void *const *targets,
                            int nreduce, int reps, int pin_cores);
+/* the same with each PE's loop split over tpp threads (contiguous element
+ * ranges, same loop shape each): npes * tpp cores, pinned to cores
+ * 0 .. npes*tpp-1 when pin_cores != 0 */
+double oracle_cpu_baseline_split(int type, int op, int npes,
+                                 const void *const *sources, void *const *targets,
+                                 int nreduce, int reps, int pin_cores, int tpp);
 
 /*
  * CPU baseline of the data-movement collectives (oracle_coll.c): kind 0

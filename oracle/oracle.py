@@ -98,6 +98,8 @@ def lib():
                                           ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_cpu_baseline.restype = ctypes.c_double
+        L.oracle_cpu_baseline_split.argtypes = L.oracle_cpu_baseline.argtypes + [ctypes.c_int]
+        L.oracle_cpu_baseline_split.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -166,18 +168,23 @@ def fold_with(fn, t, op, sources, me, PE_start, logPE_stride, PE_size):
 
 
 def cpu_baseline(t: str, op: str, sources: list, reps: int = 5,
-                 pin: bool = True) -> float:
+                 pin: bool = True, threads_per_pe: int = 1, targets: list = None) -> float:
     """Median seconds per reduce-to-all call of the reference loop shape,
-    one pthread per PE (oracle_reduce.c)."""
+    one pthread per PE (oracle_reduce.c), or threads_per_pe pthreads per PE
+    each running that shape over a contiguous part of the elements.  If
+    `targets` is a list, the PEs' result arrays are appended to it."""
     npes = len(sources)
     srcs = [np.ascontiguousarray(s, dtype=NP_DTYPE[t]) for s in sources]
     tgts = [np.empty_like(srcs[0]) for _ in range(npes)]
     sp = (ctypes.c_void_p * npes)(*[s.ctypes.data for s in srcs])
     tp = (ctypes.c_void_p * npes)(*[x.ctypes.data for x in tgts])
-    sec = lib().oracle_cpu_baseline(TYPES.index(t), OPS.index(op), npes, sp, tp,
-                                    srcs[0].size, reps, 1 if pin else 0)
+    sec = lib().oracle_cpu_baseline_split(TYPES.index(t), OPS.index(op), npes, sp, tp,
+                                          srcs[0].size, reps, 1 if pin else 0,
+                                          threads_per_pe)
     if sec < 0:
         raise ValueError(f"no cpu baseline for {t}/{op}")
+    if targets is not None:
+        targets.extend(tgts)
     return sec
 
 

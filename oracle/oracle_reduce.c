@@ -120,7 +120,7 @@ static elem_fn pick_elem(int type, int op)
 }
 
 typedef struct {
-    int type, npes, nreduce, reps, pin;
+    int type, npes, nreduce, reps, pin, tpp;  /* tpp: threads per PE */
     size_t s;
     elem_fn fn;
     const void *const *sources;
@@ -131,7 +131,7 @@ typedef struct {
 
 typedef struct {
     bl_team *t;
-    int me;
+    int me, part;  /* PE, and which of its tpp element ranges */
 } bl_arg;
 
 static double now_s(void)
@@ -141,6 +141,11 @@ static double now_s(void)
     return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
 }
 
+/* One thread of PE `me`: with tpp = 1 the whole loop of src/reductions.c
+   :79-113; with tpp > 1 PE me's loop is split over tpp threads, each running
+   the same shape (copy, barrier, 64-element getmem chunks, indirect op,
+   barrier) over a contiguous 1/tpp of the elements -- the reference's
+   algorithm on npes * tpp cores. */
 static void *bl_pe(void *p)
 {
     bl_arg *ar = (bl_arg *) p;
@@ -149,37 +154,39 @@ static void *bl_pe(void *p)
     if (t->pin) {
         cpu_set_t cs;
         CPU_ZERO(&cs);
-        CPU_SET(me % CPU_SETSIZE, &cs);
+        CPU_SET((me * t->tpp + ar->part) % CPU_SETSIZE, &cs);
         pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
     }
     const size_t s = t->s;
-    const int n = t->nreduce, nloops = n / WRK, nrem = n % WRK;
-    char *src = (char *) t->sources[me];
-    char *dst = (char *) t->targets[me];
+    const size_t lo = (size_t) t->nreduce * (size_t) ar->part / (size_t) t->tpp;
+    const size_t hi = (size_t) t->nreduce * (size_t) (ar->part + 1) / (size_t) t->tpp;
+    const size_t n = hi - lo, nloops = n / WRK, nrem = n % WRK;
+    char *src = (char *) t->sources[me] + lo * s;
+    char *dst = (char *) t->targets[me] + lo * s;
     char *pwrk = malloc(WRK * s);
     /* first touch of target by its PE */
-    memset(dst, 0, (size_t) n * s);
+    memset(dst, 0, n * s);
     for (int r = 0; r <= t->reps; r++) {
         pthread_barrier_wait(&t->bar);
         double t0 = now_s();
-        memcpy(dst, src, (size_t) n * s);           /* :79-81 */
+        memcpy(dst, src, n * s);                      /* :79-81 */
         pthread_barrier_wait(&t->bar);                /* :82 */
         for (int pe = 0; pe < t->npes; pe++) {        /* :84-111 */
             if (pe == me) continue;
-            const char *peer = (const char *) t->sources[pe]; /* same offset */
+            const char *peer = (const char *) t->sources[pe] + lo * s; /* same offset */
             size_t ti = 0, si = 0;
-            for (int k = 0; k < nloops; k++) {
+            for (size_t k = 0; k < nloops; k++) {
                 memcpy(pwrk, peer + si * s, WRK * s); /* shmem_getmem :92 */
                 for (int j = 0; j < WRK; j++, ti++)
                     t->fn(dst + ti * s, pwrk + (size_t) j * s);
                 si += WRK;
             }
-            memcpy(pwrk, peer + si * s, (size_t) nrem * s); /* :103 */
-            for (int j = 0; j < nrem; j++, ti++)
-                t->fn(dst + ti * s, pwrk + (size_t) j * s);
+            memcpy(pwrk, peer + si * s, nrem * s);    /* :103 */
+            for (size_t j = 0; j < nrem; j++, ti++)
+                t->fn(dst + ti * s, pwrk + j * s);
         }
         pthread_barrier_wait(&t->bar);                /* :113 */
-        if (me == 0) t->times[r] = now_s() - t0;
+        if (me == 0 && ar->part == 0) t->times[r] = now_s() - t0;
     }
     free(pwrk);
     return NULL;
@@ -191,26 +198,31 @@ static int cmp_d(const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
-double oracle_cpu_baseline(int type, int op, int npes,
-                           const void *const *sources, void *const *targets,
-                           int nreduce, int reps, int pin_cores)
+/* the reference loop shape with npes * tpp pthreads (tpp per PE, pinned to
+   cores 0 .. npes*tpp-1 when pin_cores); median seconds per call */
+double oracle_cpu_baseline_split(int type, int op, int npes,
+                                 const void *const *sources, void *const *targets,
+                                 int nreduce, int reps, int pin_cores, int tpp)
 {
     elem_fn fn = pick_elem(type, op);
-    if (!fn || npes < 1 || reps < 1 || nreduce < 0) return -1.0;
+    if (!fn || npes < 1 || reps < 1 || nreduce < 0 || tpp < 1) return -1.0;
     bl_team t;
     memset(&t, 0, sizeof(t));
     t.type = type; t.npes = npes; t.nreduce = nreduce; t.reps = reps; t.pin = pin_cores;
+    t.tpp = tpp;
     t.s = oracle_type_size(type); t.fn = fn; t.sources = sources; t.targets = targets;
     t.times = calloc((size_t) reps + 1, sizeof(double));
-    pthread_barrier_init(&t.bar, NULL, (unsigned) npes);
-    pthread_t *th = calloc((size_t) npes, sizeof(pthread_t));
-    bl_arg *args = calloc((size_t) npes, sizeof(bl_arg));
-    for (int i = 0; i < npes; i++) {
+    const int nth = npes * tpp;
+    pthread_barrier_init(&t.bar, NULL, (unsigned) nth);
+    pthread_t *th = calloc((size_t) nth, sizeof(pthread_t));
+    bl_arg *args = calloc((size_t) nth, sizeof(bl_arg));
+    for (int i = 0; i < nth; i++) {
         args[i].t = &t;
-        args[i].me = i;
+        args[i].me = i / tpp;
+        args[i].part = i % tpp;
         pthread_create(&th[i], NULL, bl_pe, &args[i]);
     }
-    for (int i = 0; i < npes; i++) pthread_join(th[i], NULL);
+    for (int i = 0; i < nth; i++) pthread_join(th[i], NULL);
     pthread_barrier_destroy(&t.bar);
     qsort(t.times + 1, (size_t) reps, sizeof(double), cmp_d); /* drop warm-up */
     double med = t.times[1 + reps / 2];
@@ -218,4 +230,12 @@ double oracle_cpu_baseline(int type, int op, int npes,
     free(th);
     free(args);
     return med;
+}
+
+double oracle_cpu_baseline(int type, int op, int npes,
+                           const void *const *sources, void *const *targets,
+                           int nreduce, int reps, int pin_cores)
+{
+    return oracle_cpu_baseline_split(type, op, npes, sources, targets, nreduce, reps,
+                                     pin_cores, 1);
 }

@@ -89,3 +89,21 @@ def test_cpu_baseline_runs():
     src = O.team_inputs("double", 2, 4096, 7, "unit12")
     sec = O.cpu_baseline("double", "sum", src, reps=3, pin=False)
     assert 0 < sec < 1.0
+
+
+@pytest.mark.parametrize("tpp", [1, 3, 8])
+@pytest.mark.parametrize("t,op,P", [("double", "sum", 2), ("long", "xor", 3), ("float", "min", 4),
+                                    ("int", "sum", 2)])
+def test_cpu_baseline_results(t, op, P, tpp):
+    # the timed baseline computes the reference's results: every PE's target
+    # equals the oracle's fold in that PE's order, whatever the thread split
+    # (ragged n: the parts and the 64-element chunks do not divide it)
+    n = 64 * 37 + 5
+    src = O.team_inputs(t, P, n, 11, "unit12" if t in ("double", "float") else "bits")
+    got = []
+    sec = O.cpu_baseline(t, op, src, reps=1, pin=False, threads_per_pe=tpp, targets=got)
+    assert 0 < sec < 1.0
+    want = O.to_all(t, op, src)
+    for pe in range(P):
+        assert np.array_equal(np.asarray(got[pe]).view(np.uint8),
+                              np.asarray(want[pe]).view(np.uint8)), pe
