@@ -484,6 +484,9 @@ def bench_single(args):
         e1.record(stream)
     torch.cuda.synchronize()
     kms = sorted(s.elapsed_time(e) for s, e in ev)
+    # and once the clocks have settled (launches 1-100 of a process run
+    # 1-3 % slower, tools/warm_probe.py): 100 more, one event pair
+    ksteady = span_per_launch(torch, stream, step, 100)
     B = 3 * n * 8
     res = {
         "metric": METRIC,
@@ -521,6 +524,10 @@ def bench_single(args):
         "kernel_median_us_per_launch_events": kms[len(kms) // 2] * 1e3,
         "kernel_min_us_per_launch_events": kms[0] * 1e3,
         "algorithmic_bytes_per_launch": B,
+        "after_timed_region_100_launches": {
+            "kernel_avg_us": ksteady * 1e6, "frac": B / ksteady / 1e9 / HBM_PEAK_GBS,
+            "note": "not the timed region: 100 more launches after it (event span / 100), "
+                    "once the start-of-process ramp is over"},
     }
     # the kernel the API dispatches (TEAM path), under the same roofline
     try:
