@@ -508,6 +508,12 @@ def bench_single(args):
     }
     del a, b, out
     torch.cuda.empty_cache()
+    # this box's streaming ceiling at the same footprint (copy kernel: 1 read
+    # + 1 write stream, 3*n*8 bytes moved): box-to-box spread is the memory's
+    try:
+        ceil64 = stream_ceiling(L, torch, 3 * n * 8 // 2, reps=args.steps)
+    except Exception as e:  # report, never hide
+        ceil64 = {"error": repr(e)}
     if not args.no_extra:
         try:
             res.update(extra_kernel_rates(L, torch))
@@ -528,7 +534,10 @@ def bench_single(args):
             "kernel_avg_us": ksteady * 1e6, "frac": B / ksteady / 1e9 / HBM_PEAK_GBS,
             "note": "not the timed region: 100 more launches after it (event span / 100), "
                     "once the start-of-process ramp is over"},
+        "copy_ceiling_same_bytes": ceil64,
     }
+    if "frac_of_8TBs" in ceil64:
+        res["roofline"]["frac_of_copy_ceiling"] = res["roofline"]["frac"] / ceil64["frac_of_8TBs"]
     # the kernel the API dispatches (TEAM path), under the same roofline
     try:
         res["roofline_team"] = team_kernel_rate(L, torch, n, args.steps)
