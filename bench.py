@@ -789,6 +789,31 @@ def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
     return out
 
 
+def start_watchdog(res, rank, deadline):
+    """The N > 1 line's printer and deadline: emit() prints `res` once (rank
+    0); if the run is still going after `deadline` seconds, the watchdog
+    marks the line incomplete (naming state["phase"]), prints it and ends
+    the process with status 3 -- a stalled run is never recorded as a
+    success (tests/test_bench_contract.py)."""
+    printed = threading.Lock()
+    state = {"printed": False, "phase": "setup"}
+
+    def emit():
+        with printed:
+            if rank == 0 and not state["printed"]:
+                state["printed"] = True
+                print(json.dumps(res), flush=True)
+
+    def watchdog():
+        time.sleep(deadline)
+        res["incomplete"] = f"deadline {deadline}s reached during {state['phase']}"
+        emit()
+        os._exit(3)   # a stalled run must not be recorded as a success
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    return state, emit
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -830,22 +855,7 @@ def bench_multi(args):
                    "bytes_convention": "(P+1)*nreduce*8 per step (SURVEY.md 8d aggregate)",
                    "parallelism": f"pe{world}"},
     }
-    printed = threading.Lock()
-    state = {"printed": False, "phase": "setup"}
-
-    def emit():
-        with printed:
-            if rank == 0 and not state["printed"]:
-                state["printed"] = True
-                print(json.dumps(res), flush=True)
-
-    def watchdog():
-        time.sleep(args.deadline)
-        res["incomplete"] = f"deadline {args.deadline}s reached during {state['phase']}"
-        emit()
-        os._exit(3)   # a stalled run must not be recorded as a success
-
-    threading.Thread(target=watchdog, daemon=True).start()
+    state, emit = start_watchdog(res, rank, args.deadline)
 
     # ---- the device symmetric heap: ONE contiguous virtual range per PE
     # (osgpu_heap_create: dmabuf chunks mapped into every member), holding
