@@ -427,6 +427,8 @@ def small_call_latency(n=1024, reps=300):
     for k in ("fused_team", "team", "host_fused_staged", "host_staged"):
         v = lat[f"{n}/{k}"]
         out[k + "_us"] = v["us_median"]
+        if "us_median_timed_in_c" in v:   # the loop in C, like the CPU baseline's
+            out[k + "_us_timed_in_c"] = v["us_median_timed_in_c"]
         out[k + "_correct"] = v["correct"]
     out["note"] += ("; host_* = the same call on a pinned host symmetric heap (config 1's "
                     "own placement): fused staged (one launch) vs pipelined STAGED")

@@ -737,7 +737,14 @@ def device_heap_modes(L, PES, mode, rank, world):
                 got = heap[toff:toff + n * 4].view(torch.int32).cpu().numpy()
                 ok = bool(np.array_equal(got, world * np.arange(n, dtype=np.int32)
                                          + world * (world - 1) // 2))
+                # the same call timed in C between the runtime's barriers (as
+                # the CPU baseline is timed): no Python in the loop
+                fnp = ctypes.cast(L.shmem_int_sum_to_all, ctypes.c_void_p)
+                tc = PES.pes_time_to_all(fnp, ctypes.c_void_p(dev0 + toff), ctypes.c_void_p(dev0),
+                                         n, 0, 0, world, ctypes.c_void_p(ctypes.addressof(wrk)),
+                                         ctypes.c_void_p(psync), reps)
                 lat[f"{n}/{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
+                                      "us_median_timed_in_c": tc * 1e6,
                                       "gpu_us_median": float(np.median(gpu)),
                                       "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
                                       "path": ran, "correct": ok}

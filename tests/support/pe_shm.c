@@ -21,6 +21,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #define MAXSETS 64
@@ -137,3 +138,37 @@ typedef struct {
 static pe_ops_t g_table = {pes_my_pe, pes_n_pes, pes_barrier, pes_getmem};
 
 const void *pes_ops(void) { return &g_table; }
+
+/* Per-call time of a reduce-to-all entry point timed in C, as the CPU
+ * baseline is (oracle_reduce.c: CLOCK_MONOTONIC from barrier to barrier):
+ * `reps` calls after 5 warm-up calls, each between two pes_barrier()s over
+ * the whole job; median seconds per call.  fn has the reference's signature
+ * (include/shmem/api.h: target, source, nreduce, PE_start, logPE_stride,
+ * PE_size, pWrk, pSync). */
+typedef void (*to_all_fn)(void *, void *, int, int, int, int, void *, long *);
+
+static int cmp_dbl(const void *a, const void *b)
+{
+    const double x = *(const double *) a, y = *(const double *) b;
+    return x < y ? -1 : x > y;
+}
+
+double pes_time_to_all(void *fn, void *target, void *source, int nreduce, int PE_start,
+                       int logPE_stride, int PE_size, void *pWrk, long *pSync, int reps)
+{
+    if (reps < 1) return -1.0;
+    double *t = malloc(sizeof(double) * (size_t) reps);
+    for (int r = -5; r < reps; r++) {
+        struct timespec a, b;
+        pes_barrier(0, 0, g_npes, NULL);
+        clock_gettime(CLOCK_MONOTONIC, &a);
+        ((to_all_fn) fn)(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+        pes_barrier(0, 0, g_npes, NULL);
+        clock_gettime(CLOCK_MONOTONIC, &b);
+        if (r >= 0) t[r] = (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
+    }
+    qsort(t, (size_t) reps, sizeof(double), cmp_dbl);
+    const double med = t[reps / 2];
+    free(t);
+    return med;
+}

@@ -15,6 +15,14 @@ __global__ void empty_kernel(int *p)
     if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
 }
 
+// writes seq to a host-mapped word (system scope): the host returns when it
+// sees it, without waiting for the launch to retire (the fused path's form)
+__global__ void word_kernel(unsigned long long *w, unsigned long long seq)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        __hip_atomic_store(w, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 static double median_us(int reps, const std::function<void()> &f)
 {
     std::vector<double> t(reps);
@@ -91,6 +99,27 @@ int main()
                hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, d);
                (void) hipEventRecord(ev, st);
                (void) hipEventSynchronize(ev);
+           }));
+    // launch -> the host sees a word the kernel wrote (pinned, mapped host
+    // memory), the previous launch possibly still retiring
+    unsigned long long *wh = nullptr, *wd = nullptr;
+    CK(hipHostMalloc((void **) &wh, 64, hipHostMallocMapped));
+    CK(hipHostGetDevicePointer((void **) &wd, wh, 0));
+    *wh = 0;
+    unsigned long long seq = 0;
+    printf(", \"launch_word_us\": %.3f", median_us(R, [&] {
+               ++seq;
+               hipLaunchKernelGGL(word_kernel, dim3(1), dim3(64), 0, st, wd, seq);
+               while (__atomic_load_n(wh, __ATOMIC_ACQUIRE) < seq) {
+               }
+           }));
+    CK(hipStreamSynchronize(st));
+    printf(", \"launch_word_retired_us\": %.3f", median_us(R, [&] {
+               ++seq;
+               hipLaunchKernelGGL(word_kernel, dim3(1), dim3(64), 0, st, wd, seq);
+               while (__atomic_load_n(wh, __ATOMIC_ACQUIRE) < seq) {
+               }
+               (void) hipStreamSynchronize(st);
            }));
     printf("}\n");
     return 0;
