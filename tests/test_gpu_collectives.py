@@ -226,3 +226,32 @@ def test_large_fcollect_and_broadcast_properties():
         t = tm.buf[pe * tm.H + nb:][:nb]
         want = 0xEE if pe == 1 else 2
         assert bool((t == want).all()), pe
+
+
+def _random_case(k):
+    """A seeded draw over every dimension at once: kind, width, placement
+    (device / host auto / host staged), an active set of an npes job at any
+    start and stride, nelems with the vector and chunk edges over-weighted,
+    any root, collect's per-PE counts."""
+    rng = np.random.default_rng(0xC011 + k)
+    kind = ["broadcast", "collect", "fcollect", "alltoall"][rng.integers(4)]
+    bits = int(rng.choice([32, 64]))
+    mode = MODES[rng.integers(len(MODES))]
+    log = int(rng.choice([0, 0, 1, 2]))
+    step = 1 << log
+    size = int(rng.integers(1, 8 // step + 1))
+    start = int(rng.integers(0, 8 - (size - 1) * step))
+    npes = start + (size - 1) * step + 1
+    r = rng.random()
+    nelems = int(rng.choice([0, 1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257])) if r < 0.4 \
+        else int(rng.integers(1, 3000)) if r < 0.85 else int(rng.integers(3000, 40000))
+    root = int(rng.integers(size))
+    return mode, kind, bits, (npes, start, log, size), nelems, root, int(rng.integers(1 << 30))
+
+
+@pytest.mark.parametrize("block", range(0, 120, 30))
+def test_random_collectives(block):
+    for k in range(block, block + 30):
+        mode, kind, bits, setdef, nelems, root, seed = _random_case(k)
+        with host_path(mode):
+            _run_case(mode != "device", kind, bits, setdef, nelems, root=root, seed=seed)
