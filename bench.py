@@ -109,7 +109,7 @@ def cpu_baseline(n):
     B = 2 * 3 * n * 8  # two PE results, each (K+1)*n*8
     out = {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
            "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
-                      f"2 PEs (pthreads pinned to cores 0-1), nreduce={n}, median of "
+                      f"2 PEs (pthreads pinned to the first 2 CPUs this process may use), nreduce={n}, median of "
                       f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
                       f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
     # the same loop with every PE's elements split over 8 threads: 16 cores,
@@ -121,7 +121,7 @@ def cpu_baseline(n):
     out["same_loop_16_cores"] = {
         "value": B / sec16 / GIB, "unit": "GiB/s", "cores": 2 * tpp, "ms_per_call": sec16 * 1e3,
         "sample": f"the same loop shape, each PE's elements split over {tpp} pinned threads "
-                  f"(cores 0-{2 * tpp - 1}), median of {reps16} after 1 warm-up"}
+                  f"(the first {2 * tpp} CPUs this process may use), median of {reps16} after 1 warm-up"}
     return out
 
 
@@ -141,8 +141,8 @@ def cpu_baselines_configs():
     (every PE's K = P inputs + 1 output)."""
     import oracle as O
     out = {"host_nproc": os.cpu_count(), "kind": "port",
-           "note": "oracle/oracle_reduce.c reference loop shape, pthreads pinned to cores "
-                   "0..P-1, median after 1 warm-up"}
+           "note": "oracle/oracle_reduce.c reference loop shape, pthreads pinned to the first P CPUs "
+                   "of this process's CPU set, median after 1 warm-up"}
     plans = (("config3", "long", ("and", "or", "xor"), 2, 32 << 20, "bits", 3),
              ("config5", "float", ("min", "max", "prod"), 8, 32 << 20, "unit12", 1),
              ("config4", "double", ("sum",), 8, 64 << 20, "unit12", 1))

@@ -121,6 +121,7 @@ static elem_fn pick_elem(int type, int op)
 
 typedef struct {
     int type, npes, nreduce, reps, pin, tpp;  /* tpp: threads per PE */
+    int *cpus;                                /* thread i pinned to cpus[i] */
     size_t s;
     elem_fn fn;
     const void *const *sources;
@@ -146,6 +147,19 @@ static double now_s(void)
    the same shape (copy, barrier, 64-element getmem chunks, indirect op,
    barrier) over a contiguous 1/tpp of the elements -- the reference's
    algorithm on npes * tpp cores. */
+/* the k-th CPU this process may run on (its affinity mask, e.g. a
+   container's CPU share), so pinned threads land on allowed cores */
+static int allowed_cpu(int k)
+{
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    if (sched_getaffinity(0, sizeof(cs), &cs) != 0 || CPU_COUNT(&cs) == 0) return k % CPU_SETSIZE;
+    k %= CPU_COUNT(&cs);
+    for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &cs) && k-- == 0) return c;
+    return 0;
+}
+
 static void *bl_pe(void *p)
 {
     bl_arg *ar = (bl_arg *) p;
@@ -154,7 +168,7 @@ static void *bl_pe(void *p)
     if (t->pin) {
         cpu_set_t cs;
         CPU_ZERO(&cs);
-        CPU_SET((me * t->tpp + ar->part) % CPU_SETSIZE, &cs);
+        CPU_SET(t->cpus[me * t->tpp + ar->part], &cs);
         pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
     }
     const size_t s = t->s;
@@ -213,6 +227,9 @@ double oracle_cpu_baseline_split(int type, int op, int npes,
     t.s = oracle_type_size(type); t.fn = fn; t.sources = sources; t.targets = targets;
     t.times = calloc((size_t) reps + 1, sizeof(double));
     const int nth = npes * tpp;
+    /* chosen before any thread is pinned (a pinned thread's mask is one CPU) */
+    t.cpus = calloc((size_t) nth, sizeof(int));
+    for (int i = 0; i < nth; i++) t.cpus[i] = allowed_cpu(i);
     pthread_barrier_init(&t.bar, NULL, (unsigned) nth);
     pthread_t *th = calloc((size_t) nth, sizeof(pthread_t));
     bl_arg *args = calloc((size_t) nth, sizeof(bl_arg));
@@ -227,6 +244,7 @@ double oracle_cpu_baseline_split(int type, int op, int npes,
     qsort(t.times + 1, (size_t) reps, sizeof(double), cmp_d); /* drop warm-up */
     double med = t.times[1 + reps / 2];
     free(t.times);
+    free(t.cpus);
     free(th);
     free(args);
     return med;
