@@ -111,7 +111,8 @@ def cpu_baseline(n):
            "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
                       f"2 PEs (pthreads pinned to the first 2 CPUs this process may use), nreduce={n}, median of "
                       f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
-                      f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}")}
+                      f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}, CPUs this "
+                      f"process may use {len(os.sched_getaffinity(0))}")}
     # the same loop with every PE's elements split over 8 threads: 16 cores,
     # this box's CPU share (a one-PE-per-core reference uses 2 for 2 PEs)
     tpp = 8
@@ -140,7 +141,8 @@ def cpu_baselines_configs():
     Rates: per-PE algbw nreduce*s/t and the fused-convention P*(P+1)*n*s/t
     (every PE's K = P inputs + 1 output)."""
     import oracle as O
-    out = {"host_nproc": os.cpu_count(), "kind": "port",
+    out = {"host_nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
+           "kind": "port",
            "note": "oracle/oracle_reduce.c reference loop shape, pthreads pinned to the first P CPUs "
                    "of this process's CPU set, median after 1 warm-up"}
     plans = (("config3", "long", ("and", "or", "xor"), 2, 32 << 20, "bits", 3),
