@@ -369,6 +369,34 @@ def vmm_heap_mode(L, PES, rank, world):
     return res
 
 
+def fuzz_case(k, world):
+    """Case k of the multi-process random sweep (the same on every rank)."""
+    import oracle as O
+    rng = np.random.default_rng(0xF0F0 + k)
+    t = O.TYPES[rng.integers(len(O.TYPES))]
+    ops = [op for op in O.OPS if O.has_op(t, op)]
+    op = ops[rng.integers(len(ops))]
+    stride = int(rng.choice([0, 0, 1])) if world >= 2 else 0
+    step = 1 << stride
+    size = int(rng.integers(1, (world - 1) // step + 2))
+    start = int(rng.integers(0, world - (size - 1) * step))
+    r = rng.random()
+    n = int(rng.choice([0, 1, 2, 15, 63, 64, 65, 257, 1023, 4097])) if r < 0.35 \
+        else int(rng.integers(1, 8192)) if r < 0.8 else int(rng.integers(8192, 70000))
+    s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+    ph = lambda: s * int(rng.integers(0, 16 // s if s < 16 else 2))  # noqa: E731
+    soff = 4096 + ph()
+    in_place = bool(rng.random() < 0.15)
+    toff = soff if in_place else (soff + n * s + 4095) // 4096 * 4096 + 4096 + ph()
+    dists = ["bits", "mixed", "edge"] if t in O.INT_TYPES else \
+        (["prod", "edge"] if op == "prod" else ["mixed", "edge", "wide"])
+    return dict(t=t, op=op, start=start, stride=stride, size=size, n=n, soff=soff, toff=toff,
+                in_place=in_place, dist=dists[rng.integers(len(dists))],
+                host=bool(rng.random() < 0.35),
+                path=int(rng.choice([osgpu.PATH_AUTO, osgpu.PATH_AUTO, osgpu.PATH_PULL])),
+                seed=int(rng.integers(1 << 40)))
+
+
 def device_heap_modes(L, PES, mode, rank, world):
     import time
     import torch
@@ -471,6 +499,63 @@ def device_heap_modes(L, PES, mode, rank, world):
                     sync()
             res["misaligned"] = mis
             assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
+    if mode == "fuzz":
+        # seeded random calls, the same draw on every rank: (type, op), an
+        # active subset of the job at any start and stride, nreduce mostly
+        # inside the fused one-launch range, 16-B phases of source and
+        # target, in-place, device heaps (team / pull) or the pinned host heap
+        # (fused staged / staged); every member's target against the oracle's
+        # fold in its order, non-members' targets untouched, pSync back at 0
+        hbase = PES.pes_heap(rank)
+        hbytes = (1 << 24) - (1 << 16)
+        assert L.osgpu_host_register(ctypes.c_void_p(hbase), hbytes) == 0
+        bad, paths = [], {}
+        for k in range(int(os.environ.get("MP_FUZZ_CASES", "600"))):
+            c = fuzz_case(k, world)
+            t, op, n = c["t"], c["op"], c["n"]
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            nb = n * s
+            src = O.team_inputs(t, world, n, c["seed"], c["dist"])
+            act = O.active_set(c["start"], c["stride"], c["size"])
+            raw = np.ascontiguousarray(src[rank]).view(np.uint8).reshape(-1)
+            soff, toff, host = c["soff"], c["toff"], c["host"]
+            b0 = hbase if host else dev0
+            if host:
+                if raw.size:
+                    ctypes.memmove(hbase + soff, raw.ctypes.data, raw.size)
+                if not c["in_place"]:
+                    ctypes.memset(hbase + toff, 0x5A, max(nb, 16))
+            else:
+                put(soff, src[rank])
+                if not c["in_place"]:
+                    heap[toff:toff + max(nb, 16)].fill_(0x5A)
+                torch.cuda.synchronize()
+            L.osgpu_set_path(c["path"])
+            sync()
+            if rank in act:
+                getattr(L, f"shmem_{t}_{op}_to_all")(b0 + toff, b0 + soff, n, c["start"],
+                                                     c["stride"], c["size"], wrk, psync)
+                ran = osgpu.last_path()
+                paths[ran] = paths.get(ran, 0) + 1
+                got = (np.frombuffer(ctypes.string_at(hbase + toff, nb), np.uint8) if host
+                       else heap[toff:toff + nb].cpu().numpy())
+                if t == "longdouble":
+                    got = got.reshape(-1, 16)[:, :10].reshape(-1)
+                want = O.to_all(t, op, src, c["start"], c["stride"], c["size"])[rank]
+                if not np.array_equal(O.value_bytes(O.from_value_bytes(t, got)),
+                                      O.value_bytes(want)):
+                    bad.append([k, "target", ran])
+                if any(ctypes.string_at(psync, 1024)):
+                    bad.append([k, "pSync"])
+            elif not c["in_place"]:
+                tg = (np.frombuffer(ctypes.string_at(hbase + toff, max(nb, 16)), np.uint8)
+                      if host else heap[toff:toff + max(nb, 16)].cpu().numpy())
+                if not (tg == 0x5A).all():
+                    bad.append([k, "non-member target"])
+            sync()
+        L.osgpu_set_path(osgpu.PATH_AUTO)
+        assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
+        res["fuzz_bad"], res["fuzz_paths"] = bad, paths
     if mode == "timeout":
         # a member that never enters the call: after one good fused call,
         # rank 0 calls alone; the device barrier must time out and be
@@ -913,7 +998,8 @@ def main():
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
-            "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle", "heapleak"):
+            "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle", "heapleak",
+            "fuzz"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -968,7 +1054,7 @@ def main():
         res["out"] = out
     if mode == "mixpush":
         res.update(mixpush_mode(L, PES, rank, world))
-    if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout", "late"):
+    if mode in ("golden", "goldenhost", "collgolden", "latency", "timeout", "late", "fuzz"):
         res.update(device_heap_modes(L, PES, mode, rank, world))
     if mode == "vmm":
         res.update(vmm_heap_mode(L, PES, rank, world))

@@ -243,6 +243,28 @@ def test_fused_path_golden_processes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_random_calls_processes(tmp_path):
+    """Four processes on cuda:0, 600 seeded random calls drawn the same on
+    every rank (tests/support/mp_worker.py fuzz_case): any (type, op), active
+    subsets at any start and stride, nreduce mostly inside the one-launch
+    range, 16-B phases, in-place, device heaps and the pinned host heap.
+    Every member's target bit-exact against the oracle's fold in its order,
+    non-members untouched, pSync reset; the one-launch paths (device
+    barriers) and the host-barrier paths are both exercised."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("fuzz", 4, tmp_path)
+    paths = {}
+    for r in res:
+        assert r["fuzz_bad"] == [], (r["rank"], r["fuzz_bad"][:5])
+        for k, v in r["fuzz_paths"].items():
+            paths[k] = paths.get(k, 0) + v
+    for p in ("fused_team", "fused_pull", "fused_staged", "team", "pull"):
+        assert paths.get(p, 0) > 0, paths
+
+
+@pytest.mark.gpu
 def test_fused_staged_golden_processes(tmp_path):
     """The golden cases with at most 4 PEs on HOST symmetric heaps (the
     reference's placement: a shared-memory heap, pinned on every PE), four
