@@ -9,9 +9,14 @@ SO = os.path.join(HERE, "libpe_shm.so")
 
 
 def build():
+    """(Re)build libpe_shm.so when pe_shm.c is newer.  Several PE processes
+    may get here at once: each compiles to its own file and renames it into
+    place, so no process ever loads a half-written library."""
     src = os.path.join(HERE, "pe_shm.c")
     if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
-        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SO, src, "-lrt"], check=True)
+        tmp = f"{SO}.{os.getpid()}.tmp"
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", tmp, src, "-lrt"], check=True)
+        os.replace(tmp, SO)
 
 
 def load():
