@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-api", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=64 << 20,
                     help="nreduce of the CPU-baseline sample")
+    ap.add_argument("--dry-ranks", action="store_true",
+                    help="N>1 launcher check without the GPU (tests/test_bench_contract.py)")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -407,20 +410,24 @@ def extra_kernel_rates(L, torch):
     return out
 
 
-def small_call_latency(n=1024, reps=300):
+def small_call_latency(n=1024, reps=300, sizes=(1024, 4096, 8192, 16384, 32768, 65536)):
     """BASELINE config 1's shape (shmem_int_sum_to_all, nreduce = 1 Ki, 2 PEs)
     with one PROCESS per PE, both on this GPU (IPC device heaps, the
     shared-memory PE runtime of tests/support/pe_shm.c): median per call of
     the fused one-launch path (device-side barriers) and of the host-barrier
     path, timed barrier to barrier (tools/mp_latency.py), next to the
-    reference's loop shape on 2 host cores."""
+    reference's loop shape on 2 host cores.  The same at larger sizes gives
+    the crossover: the smallest nreduce at which the drop-in beats the
+    reference's loop (src/reductions.c:79-113) -- below it, it is slower."""
     import subprocess
     import oracle as O
-    env = dict(os.environ, MP_WORLDS="2", MP_SIZES=str(n), MP_REPS=str(reps))
+    sizes = sorted(set(sizes) | {n})
+    env = dict(os.environ, MP_WORLDS="2", MP_SIZES=",".join(map(str, sizes)),
+               MP_REPS=str(reps))
     env.pop("RANK", None)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mp_latency.py")], env=env,
-                       capture_output=True, text=True, timeout=240)
+                       capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         return {"error": (r.stdout + r.stderr)[-400:]}
     lat = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["latency"]
@@ -434,8 +441,32 @@ def small_call_latency(n=1024, reps=300):
         out[k + "_correct"] = v["correct"]
     out["note"] += ("; host_* = the same call on a pinned host symmetric heap (config 1's "
                     "own placement): fused staged (one launch) vs pipelined STAGED")
-    src = O.team_inputs("int", 2, n, 5, "bits")
-    out["cpu_reference_loop_us"] = O.cpu_baseline("int", "sum", src, reps=2000, pin=True) * 1e6
+    cpu = {}
+    for m in sizes:
+        src = O.team_inputs("int", 2, m, 5, "bits")
+        cpu[m] = O.cpu_baseline("int", "sum", src, reps=max(50, min(2000, int(2e7 / m))),
+                                pin=True) * 1e6
+    out["cpu_reference_loop_us"] = cpu[n]
+    sweep = [{"nreduce": m, "cpu_reference_loop_us": cpu[m],
+              "fused_team_us": lat[f"{m}/fused_team"]["us_median"],
+              "host_fused_staged_us": lat[f"{m}/host_fused_staged"]["us_median"]}
+             for m in sizes]
+    out["sweep"] = sweep
+
+    def crossover(key):
+        # smallest size from which on the GPU call is faster at every larger size
+        for i, rec in enumerate(sweep):
+            if all(x[key] < x["cpu_reference_loop_us"] for x in sweep[i:]):
+                return rec["nreduce"]
+        return None
+    best = min(out["fused_team_us"], out["host_fused_staged_us"])
+    out["crossover_elements"] = {"device_heaps_fused": crossover("fused_team_us"),
+                                 "pinned_host_heaps_fused": crossover("host_fused_staged_us")}
+    out["slower_than_reference_loop"] = best > cpu[n]
+    out["ratio_to_reference_loop"] = best / cpu[n]
+    out["crossover_note"] = ("below crossover_elements the drop-in's small call (kernel launch "
+                             "+ device barriers, >= ~11 us) is slower than the reference's CPU "
+                             "loop (kind: port, memcpy getmem, no UCX); from there on faster")
     return out
 
 
@@ -591,7 +622,10 @@ def _log(rank, msg):
 def _sample_parity(rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15, t="double"):
     """Bit-exact check of this PE's target on a sample of elements: every
     rank contributes its source at the sampled indices (gloo), the oracle
-    folds them in this PE's order (src/reductions.c:79-111)."""
+    folds them in this PE's order (src/reductions.c:79-111).  For float /
+    double also the largest difference in ulps (same-sign results: the
+    distance of the bit patterns) -- the measure of DESIGN.md 3's RCCL
+    tolerance."""
     import numpy as np
     import torch
     import oracle as O
@@ -603,15 +637,75 @@ def _sample_parity(rank, world, src, tgt, n, fn_op, dist, nsamp=1 << 15, t="doub
     srcs = [a.numpy() for a in allv]
     want = O.fold_with(O.op_elementwise, t, fn_op, srcs, rank, 0, 0, world)
     got = tgt[idx.to(tgt.device)].cpu().numpy()
-    ui = np.uint64 if t == "double" else np.uint32
+    isz = got.dtype.itemsize
+    ui = {2: np.uint16, 4: np.uint32, 8: np.uint64}[isz]
     bad = int(np.count_nonzero(got.view(ui) != want.view(ui)))
-    rel = float(np.max(np.abs(got - want) / np.abs(want))) if nsamp else 0.0
-    local = {"checked": nsamp, "bit_mismatches": bad, "max_rel_err": rel}
+    local = {"checked": nsamp, "bit_mismatches": bad}
+    if t in ("float", "double"):
+        si = {4: np.int32, 8: np.int64}[isz]
+        rel = float(np.max(np.abs(got - want) / np.abs(want))) if nsamp else 0.0
+        same = np.signbit(got) == np.signbit(want)
+        d = np.abs(got.view(si).astype(np.int64)[same] - want.view(si).astype(np.int64)[same])
+        local["max_rel_err"] = rel
+        local["max_ulp"] = (int(d.max()) if d.size else 0) if bool(same.all()) else None
     allp = [None] * world
     dist.all_gather_object(allp, local)
-    return {"checked_per_pe": nsamp,
-            "bit_mismatches": sum(p["bit_mismatches"] for p in allp),
-            "max_rel_err": max(p["max_rel_err"] for p in allp)}
+    out = {"checked_per_pe": nsamp,
+           "bit_mismatches": sum(p["bit_mismatches"] for p in allp)}
+    if t in ("float", "double"):
+        out["max_rel_err"] = max(p["max_rel_err"] for p in allp)
+        ulps = [p["max_ulp"] for p in allp]
+        out["max_ulp"] = None if None in ulps else max(ulps)
+    return out
+
+
+def _rccl_tolerance(parity, world):
+    """RCCL's FP sum of same-sign inputs is within 2(P-1) ulp
+    of the reference's per-PE fold."""
+    bound = 2 * (world - 1)
+    mu = parity.get("max_ulp")
+    return {"bound_ulp": bound, "max_ulp": mu,
+            "within_tolerance": mu is not None and mu <= bound,
+            "rule": "same-sign sum: |RCCL - reference order| <= 2(P-1) ulp (DESIGN.md 3)"}
+
+
+def _rccl_integer_legs(L, osgpu, torch, dist, rank, world, dev, psync, nint, steps=3):
+    """The AUTOMATIC path's RCCL dispatch for integer (type, op)s (no heap
+    holds these arrays, so shmem_reduce.cpp sends them to ncclAllReduce):
+    results must be bit-exact against the oracle's per-PE fold, wrap-around
+    included -- int sum near INT_MAX, long prod of full-range odd values,
+    int min and long max over the full range."""
+    legs = (("int", "sum", torch.int32, lambda x, gen: x.random_(2**31 - 4096, 2**31 - 1,
+                                                                 generator=gen)),
+            ("long", "prod", torch.int64, lambda x, gen: x.random_(-2**62, 2**62,
+                                                                   generator=gen).bitwise_or_(1)),
+            ("int", "min", torch.int32, lambda x, gen: x.random_(-2**31, 2**31 - 1,
+                                                                 generator=gen)),
+            ("long", "max", torch.int64, lambda x, gen: x.random_(-2**63, 2**63 - 1,
+                                                                  generator=gen)))
+    wrk = (ctypes.c_long * 64)()
+    out = {"nreduce": nint, "path_mode": "auto (arrays outside every heap)"}
+    L.osgpu_set_path(osgpu.PATH_AUTO)
+    gen = torch.Generator(device=dev).manual_seed(7000 + rank)
+    for t, op, dt, fill in legs:
+        s_ = torch.empty(nint, dtype=dt, device=dev)
+        d_ = torch.empty(nint, dtype=dt, device=dev)
+        fill(s_, gen)
+        torch.cuda.synchronize()
+        fn = getattr(L, f"shmem_{t}_{op}_to_all")
+
+        def step():
+            fn(d_.data_ptr(), s_.data_ptr(), nint, 0, 0, world, wrk, psync)
+
+        tt = _timed(step, steps, 1, dist, torch)
+        par = _sample_parity(rank, world, s_, d_, nint, op, dist, t=t)
+        out[f"{t}_{op}"] = {"path": osgpu.last_path(), "ms_per_call": tt / steps * 1e3,
+                            "algbw_GiBs": nint * s_.element_size() * steps / tt / GIB,
+                            "parity_vs_oracle": par,
+                            "bit_exact": par["bit_mismatches"] == 0}
+        del s_, d_
+    torch.cuda.empty_cache()
+    return out
 
 
 def _timed(step, steps, warmup, dist, torch):
@@ -819,20 +913,21 @@ def start_watchdog(res, rank, deadline):
 
 
 def bench_multi(args):
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    # ranks sharing a GPU (a rehearsal): the hardware-queue cap must be in
+    # the environment before this process's first HIP call, so the devices
+    # are counted without HIP (launch_ranks passes BENCH_NDEV; under
+    # torch.distributed.run a child process counts them)
+    ndev = device_count_without_hip()
+    cap = hw_queue_cap(world, ndev)
+    if cap is not None:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", cap)
     import torch
     import torch.distributed as dist
     import osgpu
     from support import peshm
-    rank = int(os.environ["RANK"])
-    world = int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
-    ndev = torch.cuda.device_count()
-    if 0 < ndev < world:
-        # ranks sharing a GPU (a rehearsal): at most 16 hardware queues on
-        # it between them, or its scheduler time-slices them in milliseconds
-        # (INTEGRATION.md); set before the first HIP call of this process
-        per_gpu = -(-world // ndev)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(1, 16 // per_gpu)))
     dev_id = local % max(ndev, 1)
     torch.cuda.set_device(dev_id)
     dev = torch.device("cuda", dev_id)
@@ -859,6 +954,10 @@ def bench_multi(args):
                    "bytes_convention": "(P+1)*nreduce*8 per step (SURVEY.md 8d aggregate)",
                    "parallelism": f"pe{world}"},
     }
+    res["launch"] = {"launcher": "bench.py (own ranks)" if "BENCH_NDEV" in os.environ
+                     else "external (torch.distributed.run)",
+                     "gpus_visible": ndev, "ranks_per_gpu": -(-world // max(ndev, 1)),
+                     "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
     state, emit = start_watchdog(res, rank, args.deadline)
 
     # ---- the device symmetric heap: ONE contiguous virtual range per PE
@@ -881,6 +980,30 @@ def bench_multi(args):
     except Exception as e:  # collective: the same verdict on every rank
         vmm_err = repr(e)[:300]
     team_ok = heap_base is not None
+    # ---- preflight: every cross-process mapping checked with patterns at
+    # both ends of every heap chunk, staging area and flag area, host copy
+    # then copy kernel, BEFORE any kernel uses them (osgpu_preflight); a bad
+    # mapping becomes a named entry here instead of a GPU fault later
+    state["phase"] = "preflight"
+    staging_ok = True
+    try:
+        prc, prep = osgpu.preflight(heap_base, 0, 0, world, psync.value)
+        allrep = [None] * world
+        dist.all_gather_object(allrep, {"rc": prc, "report": prep})
+        res["heap_preflight"] = {str(r): x["report"] for r, x in enumerate(allrep)}
+        heap_bad = any("heap" in str(v.get("status", "")) for x in allrep
+                       for k, v in x["report"].items() if isinstance(v, dict))
+        staging_ok = not any("staging" in str(v.get("status", "")) for x in allrep
+                             for k, v in x["report"].items() if isinstance(v, dict))
+        res["heap_preflight_ok"] = all(x["rc"] == 0 for x in allrep)
+        if heap_bad and team_ok:
+            # do not run kernels through a mapping that failed its probe
+            res["heap_error"] = "preflight: some heap chunk mapping failed (heap_preflight)"
+            team_ok = False
+    except Exception as e:  # report, never hide
+        res["heap_preflight"] = {"error": repr(e)[:300]}
+        res["heap_preflight_ok"] = False
+    _log(rank, f"preflight ok={res.get('heap_preflight_ok')}")
     if team_ok:
         hsrc = osgpu.device_view(heap_base, seg_bytes)
         htgt = osgpu.device_view(heap_base + seg_bytes, seg_bytes)
@@ -1043,8 +1166,10 @@ def bench_multi(args):
             t2 = _timed(step, args.steps, args.warmup, dist, torch)
             rr = {"value": args.steps * B / t2 / GIB, "ms_per_step": t2 / args.steps * 1e3,
                   "algbw_GiBs": n * 8 * args.steps / t2 / GIB,
+                  "path": osgpu.last_path(),
                   "parity_vs_reference_order": _sample_parity(rank, world, src, tgt, n, "sum",
                                                               dist)}
+            rr["tolerance"] = _rccl_tolerance(rr["parity_vs_reference_order"], world)
             res["rccl"] = rr
             if res["value"] is None:   # no IPC: RCCL carries the line, flagged
                 res["value"], res["ms_per_step"] = rr["value"], rr["ms_per_step"]
@@ -1052,6 +1177,19 @@ def bench_multi(args):
             _log(rank, "rccl done")
         except Exception as e:  # reported, never hidden
             res["rccl"] = {"error": repr(e)[:300]}
+            if 0 < ndev < world:
+                res["rccl"]["note"] = ("ranks share a GPU in this run: RCCL refuses more than "
+                                       "one rank per GPU, so no RCCL leg can run here")
+        # the automatic path's integer dispatch to RCCL, bit-exact vs the oracle
+        if rccl_ok:
+            state["phase"] = "rccl_integer"
+            try:
+                res["rccl_integer_auto"] = _rccl_integer_legs(
+                    L, osgpu, torch, dist, rank, world, dev, psync, min(n, 16 << 20))
+                _log(rank, "rccl integer legs done")
+            except Exception as e:  # reported, never hidden
+                res["rccl_integer_auto"] = {"error": repr(e)[:300]}
+            L.osgpu_set_path(osgpu.PATH_RCCL)
     # ---- BASELINE config 4: double sum, nreduce = 1 Gi (8 GiB per PE) over
     # every GPU.  Exact path: the team kernel over the VMM heaps (each GPU
     # folds its shard of every PE's target in that PE's own order); beside
@@ -1085,6 +1223,9 @@ def bench_multi(args):
                             "xgmi_in_GBs_per_gpu": 3 * 2 * (world - 1) * (n4 * 8 // world) / tt / 1e9,
                             "parity_vs_reference_order":
                                 _sample_parity(rank, world, s4, t4, n4, "sum", dist)}
+                if name == "rccl":
+                    c4[name]["tolerance"] = _rccl_tolerance(
+                        c4[name]["parity_vs_reference_order"], world)
                 _log(rank, f"config4 {name} done")
             L.osgpu_set_path(osgpu.PATH_AUTO)
             del s4, t4
@@ -1160,7 +1301,18 @@ def bench_multi(args):
     if team_ok and not args.no_extra:
         state["phase"] = "xgmi_probe"
         try:
-            res["xgmi_probe"] = _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes)
+            xp = _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes)
+            res["xgmi_probe"] = xp
+            link = max(xp["pull_reads_GBs_per_link"], xp["push_writes_GBs_per_link"])
+            rf = res.get("roofline")
+            if rf is not None and rf.get("bound") == "xgmi":
+                rf["peak_assumed_link_GBs"] = XGMI_LINK_GBS
+                rf["peak_measured_link_GBs"] = link
+                rf["peak_measured_how"] = ("xgmi_probe: the copy kernel moving one chunk per "
+                                           "peer on every GPU at once, best of remote reads / "
+                                           "remote writes, per link per direction")
+                if ndev >= world:
+                    rf["frac_of_measured_peak"] = rf["achieved"] / ((world - 1) * link)
             _log(rank, "xgmi probe done")
         except Exception as e:
             res["xgmi_probe"] = {"error": repr(e)[:300]}
@@ -1190,9 +1342,138 @@ def bench_multi(args):
     dist.destroy_process_group()
 
 
+def device_count_without_hip():
+    """GPUs this job may use, counted WITHOUT initialising HIP in this
+    process: GPU_MAX_HW_QUEUES (and anything else HIP reads once) must be in
+    a rank's environment before its first HIP call, and the launching parent
+    must never touch the GPU at all (it only starts and waits for children).
+    BENCH_NDEV (set by the launcher for its ranks) wins; otherwise a child
+    process asks torch."""
+    v = os.environ.get("BENCH_NDEV")
+    if v is not None:
+        return int(v)
+    import subprocess
+    r = subprocess.run([sys.executable, "-c",
+                        "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def hw_queue_cap(world, ndev):
+    """Ranks sharing a GPU (a rehearsal on fewer GPUs than ranks): at most
+    16 hardware queues on it between them, or its scheduler time-slices
+    them in milliseconds (INTEGRATION.md, profiles/r02_mp_latency_hwq.jsonl).
+    None when every rank has its own GPU (HIP's default stays)."""
+    if 0 < ndev < world:
+        per_gpu = -(-world // ndev)
+        return str(max(1, 16 // per_gpu))
+    return None
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`python bench.py --gpus N` with no RANK in the environment: start the
+    N ranks here, one child process per GPU (the reference's launcher also
+    starts its own PEs, src/shmemc/oshrun.in:4), with RANK / LOCAL_RANK /
+    WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as
+    torch.distributed.run would.  This process never touches the GPU (no
+    HIP call, no exec after one): it relays rank 0's output and exits with
+    the first non-zero rank status, or 1 when no rank printed a JSON line.
+    A rank that fails ends the others after a grace period (they may be
+    waiting for it in a collective)."""
+    import subprocess
+    world = max(args.gpus, int(os.environ.get("WORLD_SIZE", "1")))
+    ndev = device_count_without_hip()
+    env0 = dict(os.environ, WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                BENCH_NDEV=str(ndev), PYTHONUNBUFFERED="1")
+    cap = hw_queue_cap(world, ndev)
+    if cap is not None and "GPU_MAX_HW_QUEUES" not in os.environ:
+        env0["GPU_MAX_HW_QUEUES"] = cap
+    procs = []
+    for r in range(world):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=subprocess.PIPE, text=True))
+    lines = {r: [] for r in range(world)}
+
+    def relay(r, p):
+        for line in p.stdout:
+            lines[r].append(line)
+            if r == 0:                      # rank 0's line is the bench line
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.write(f"[bench rank {r} stdout] {line}")
+    readers = [threading.Thread(target=relay, args=(r, p), daemon=True)
+               for r, p in enumerate(procs)]
+    for t in readers:
+        t.start()
+    limit = time.time() + args.deadline + 300      # the ranks' own watchdog fires first
+    grace = float(os.environ.get("BENCH_RANK_GRACE_S", "60"))
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        now = time.time()
+        if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+            failed_at = now
+        if now > limit or (failed_at is not None and now - failed_at > grace):
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    for t in readers:
+        t.join(timeout=10)
+    codes = [p.returncode for p in procs]
+    bad = [c for c in codes if c != 0]
+    has_line = any(l.startswith("{") for l in lines[0])
+    if bad or not has_line:
+        sys.stderr.write(f"[bench launcher] rank exit codes {codes}; "
+                         f"rank 0 printed {'a' if has_line else 'no'} JSON line\n")
+    return bad[0] if bad else (0 if has_line else 1)
+
+
+def dry_rank(args):
+    """--dry-ranks: what a rank of launch_ranks() sees, without the GPU:
+    join the gloo group through MASTER_ADDR/PORT, gather every rank's
+    plumbing, rank 0 prints it as one JSON line (tests/test_bench_contract.py).
+    --dry-fail-rank R: rank R exits with status 7 after the gather."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    mine = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                            "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                                            "GPU_MAX_HW_QUEUES", "BENCH_NDEV")}
+    mine["pid"] = os.getpid()
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry": True, "n_gpus": world, "ranks": allr}), flush=True)
+    if rank == args.dry_fail_rank:
+        sys.exit(7)
+
+
 def main():
     args = parse()
-    if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    multi = args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if multi and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.dry_ranks:
+        dry_rank(args)
+    elif multi:
         bench_multi(args)
     else:
         bench_single(args)

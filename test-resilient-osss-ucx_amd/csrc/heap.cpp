@@ -39,6 +39,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -53,6 +54,7 @@ namespace {
 constexpr int kHeapPsync = 16;       // pSync[16..] during setup only (cf. runtime.cpp)
 constexpr int kFdBatch = 64;         // descriptors per SCM_RIGHTS message
 constexpr int kSetupTimeoutMs = 120000;
+constexpr int kMaxHeapSegment = 255; // osgpu_heap_register_segment's limit
 
 struct Mapping {                     // one heap as mapped in this process
     int pe = -1;
@@ -80,7 +82,8 @@ std::vector<Heap *> g_heaps;
 // Destroyed heaps that hold chunks imported from other processes: their HBM
 // is not returned before the process exits on this ROCm, so
 // they are kept, fully mapped, and handed back when the same member set
-// creates a heap of the same size again (every member agrees on it).
+// creates a heap of at most that size again (a prefix of the kept range is
+// registered; every member agrees on which kept heap).
 std::vector<Heap *> g_pool;
 
 // what a PE publishes in pSync[16..] during osgpu_heap_create
@@ -331,17 +334,19 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     const size_t chunk = std::min(heap_chunk_bytes(gran), total);
     for (int i = 0; i < PE_size; i++) H->members.push_back(c.pe_at(i));
 
-    // a kept heap of this member set and size, if every member has one from
-    // the same creation: register it again instead of making a new one
+    // A kept heap of this member set at least this size, if every member has
+    // one from the same creation: register its first `total` bytes again
+    // instead of making a new one (the smallest that fits, so a job that
+    // alternates sizes holds at most its largest heap per member set).  The
+    // candidate must be THIS PE's: PE threads of one process share the pool.
     HeapMsg *mine = reinterpret_cast<HeapMsg *>(pSync + kHeapPsync);
     Heap *cand = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_hmu);
         for (Heap *k : g_pool)
-            if (k->members == H->members && k->own.bytes == total && k->own.device == dev) {
+            if (k->pe == c.me && k->members == H->members && k->own.device == dev &&
+                k->own.bytes >= total && (!cand || k->own.bytes < cand->own.bytes))
                 cand = k;
-                break;
-            }
     }
     memset(mine, 0, sizeof(*mine));
     mine->nonce = cand ? cand->key : 0;
@@ -359,6 +364,13 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     }
     barrier(c);  // every member has read every message of this phase
     memset(mine, 0, sizeof(*mine));
+    // every member computes the same rseg: the same verdict everywhere
+    if (rseg > kMaxHeapSegment) {
+        set_err("%s: the heap registry is full (segment %d > %d): destroy heaps first", where,
+                rseg, kMaxHeapSegment);
+        delete H;
+        return OSGPU_ENOMEM;
+    }
     if (reuse) {
         {
             std::lock_guard<std::mutex> lk(g_hmu);
@@ -366,13 +378,13 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             cand->seg = rseg;
             g_heaps.push_back(cand);
         }
-        for (int i = 0; i < PE_size; i++)
-            osgpu_heap_register_segment(c.pe_at(i), rseg, cand->member_base[i],
-                                        cand->member_bytes[i]);
+        for (int i = 0; i < PE_size; i++)  // cannot fail: arguments checked above
+            (void) osgpu_heap_register_segment(c.pe_at(i), rseg, cand->member_base[i],
+                                               std::min(total, cand->member_bytes[i]));
         delete H;
         *base_out = cand->own.base;
-        DBG("%s PE %d: kept heap %p of %zu B registered again (segment %d)", where, c.me,
-            (void *) cand->own.base, total, rseg);
+        DBG("%s PE %d: kept heap %p of %zu B registered again for %zu B (segment %d)", where,
+            c.me, (void *) cand->own.base, cand->own.bytes, total, rseg);
         return OSGPU_OK;
     }
     std::vector<int> fds;
@@ -380,20 +392,34 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     H->own.device = dev;
     H->own.bytes = total;
     H->own.len = chunk_lens(total, chunk);
+    bool nomem = false;  // this member's failure is a lack of device memory
     {  // more than the device has free cannot succeed: fail at once instead
        // of creating chunks until the HBM runs out
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess && total > fr) {
-            set_err("%s: %zu B requested, %zu B free on device %d", where, total, fr, dev);
+            size_t kept = 0;
+            {
+                std::lock_guard<std::mutex> lk(g_hmu);
+                for (Heap *k : g_pool)
+                    if (k->own.device == dev) kept += k->own.bytes;
+            }
+            set_err("%s: out of device memory: %zu B requested, %zu B free on device %d "
+                    "(%zu B held by destroyed heaps kept for reuse: a later heap of the same "
+                    "member set up to their size reuses them; their HBM returns at exit)",
+                    where, total, fr, dev, kept);
             ok = false;
+            nomem = true;
         }
         (void) hipGetLastError();
     }
     for (size_t k = 0; ok && k < H->own.len.size(); k++) {
         hipMemGenericAllocationHandle_t h;
         if (hipMemCreate(&h, H->own.len[k], &prop, 0) != hipSuccess) {
-            set_err("%s: hipMemCreate(%zu B) failed", where, H->own.len[k]);
+            set_err("%s: out of device memory: hipMemCreate(%zu B) failed", where,
+                    H->own.len[k]);
+            (void) hipGetLastError();
             ok = false;
+            nomem = true;
             break;
         }
         H->own.h.push_back(h);
@@ -451,6 +477,35 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         if (msg[i].bytes <= 0) ok = false;
     }
     for (int i = 0; i < PE_size; i++) H->seg = std::max(H->seg, (int) msg[i].seg);
+    // Every member reads the same messages, so the checks below give the
+    // same verdict on every member.
+    //  * the registry has room for the segment;
+    //  * no mixed topology: a process holding several PE threads AND
+    //    members in other processes would import each remote heap once per
+    //    thread, into ranges only that thread's device may access, and the
+    //    process-global registry would keep whichever thread wrote last
+    //    (a GPU fault for the others).  Threads only, or one PE per process.
+    bool refused = false;
+    if (H->seg > kMaxHeapSegment) {
+        set_err("%s: the heap registry is full (segment %d > %d): destroy heaps first", where,
+                H->seg, kMaxHeapSegment);
+        refused = true;
+    }
+    {
+        std::vector<long> pids;
+        bool shared = false;
+        for (int i = 0; i < PE_size; i++) {
+            if (std::find(pids.begin(), pids.end(), msg[i].pid) != pids.end()) shared = true;
+            else pids.push_back(msg[i].pid);
+        }
+        if (shared && pids.size() > 1) {
+            set_err("%s: unsupported topology: %zu processes, some holding several PEs of the "
+                    "active set; use one PE per process, or PE threads of one process only",
+                    where, pids.size());
+            refused = true;
+        }
+    }
+    if (refused) ok = false;
     // members that are threads of this process on another GPU use my range
     // directly: their devices need access to it too (only theirs -- a grant
     // binds this process to that GPU, which one-process-per-GPU jobs never
@@ -567,7 +622,8 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     }
     // every member's verdict; after this barrier every member has finished
     // importing, so no one connects any more: the server can stop
-    mine->status = ok ? 1 : 2;
+    // 1 ok, 2 failed, 3 failed for lack of device memory
+    mine->status = ok ? 1 : (nomem ? 3 : 2);
     barrier(c);
     stop.store(true);
     if (server.joinable()) server.join();
@@ -575,12 +631,14 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     for (int fd : fds) close(fd);
     DBG("%s PE %d: served %d of %d, ok=%d", where, c.me, served.load(), expected, (int) ok);
     bool all_ok = ok;
+    int nomem_pe = nomem ? c.me : -1;
     for (int i = 0; i < PE_size; i++) {
         const int pe = c.pe_at(i);
         if (pe == c.me) continue;
         long st = 0;
         c.ops.getmem(&st, &mine->status, sizeof(long), pe);
         all_ok = all_ok && st == 1;
+        if (st == 3 && nomem_pe < 0) nomem_pe = pe;
     }
     barrier(c);
     memset(mine, 0, sizeof(*mine));  // pSync back to SHMEM_SYNC_VALUE
@@ -588,12 +646,19 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         for (Mapping &m : H->peers) unmap(m);
         unmap(H->own);
         delete H;
+        if (refused) return OSGPU_EINVAL;  // every member refused the same way
+        if (nomem_pe >= 0) {
+            if (!nomem)
+                set_err("%s: PE %d is out of device memory for its heap", where, nomem_pe);
+            return OSGPU_ENOMEM;
+        }
         if (ok) set_err("%s: another member failed to create or map its heap", where);
         return OSGPU_EPEER;
     }
     unsigned long long key = 0x9e3779b97f4a7c15ull;  // the same on every member
     for (int i = 0; i < PE_size; i++) {
-        osgpu_heap_register_segment(c.pe_at(i), H->seg, base[i], (size_t) msg[i].bytes);
+        // cannot fail: base and size checked, segment within the registry
+        (void) osgpu_heap_register_segment(c.pe_at(i), H->seg, base[i], (size_t) msg[i].bytes);
         H->member_base.push_back(base[i]);
         H->member_bytes.push_back((size_t) msg[i].bytes);
         key = (key ^ (unsigned long long) msg[i].pid) * 0x100000001b3ull;
@@ -637,4 +702,204 @@ extern "C" int osgpu_heap_destroy(void *base)
     unmap(H->own);
     delete H;
     return OSGPU_OK;
+}
+
+// ---------------------------------------------------------------------
+// osgpu_preflight: prove every cross-process mapping of a job before its
+// first collective touches it.  A mapping that is wrong (an import that
+// failed silently, a peer range this GPU may not access, staging opened on
+// the wrong allocation) otherwise first shows up as a GPU fault inside a
+// team kernel, with no hint of which peer or chunk.  Each member writes a
+// pattern that names (PE, region, chunk, end) into 64 B at both ends of
+//   * every chunk of its heap made by osgpu_heap_create (if heap_base),
+//   * its STAGED staging area of this active set (if the runtime has
+//     shmem_getmem; the staging set is made here when it does not exist),
+//   * word 31 (unused by the protocol) of its device-barrier flag area
+//     (members in distinct processes only),
+// then every member reads every peer's patterns through ITS OWN mapping:
+// first with a host copy (hipMemcpy), then -- only where that matched --
+// with the copy kernel (copy.hip, the code path of the collectives).
+// ---------------------------------------------------------------------
+
+namespace {
+
+struct Probe {                // one 64-B block to check on a peer
+    const char *region;       // "heap" / "staging" / "flags"
+    int chunk;                // chunk index (heap), 0 otherwise
+    int end;                  // 0 low end, 1 high end
+    const char *addr;         // the peer's block as mapped in this process
+    size_t bytes;             // 64, or 8 for the flag word
+};
+
+void pattern(unsigned long long *w, size_t words, int pe, int region, int chunk, int end)
+{
+    unsigned long long x = 0x243f6a8885a308d3ull ^ ((unsigned long long) pe << 40) ^
+                           ((unsigned long long) region << 32) ^
+                           ((unsigned long long) chunk << 8) ^ (unsigned long long) end;
+    for (size_t j = 0; j < words; j++) {  // splitmix64
+        x += 0x9e3779b97f4a7c15ull;
+        unsigned long long z = x;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        w[j] = z ^ (z >> 31);
+    }
+}
+
+int region_code(const char *r) { return r[0] == 'h' ? 1 : r[0] == 's' ? 2 : 3; }
+
+// chunk layout of the heap whose own range starts at `base` (this process)
+bool own_chunks(const char *base, std::vector<size_t> *len)
+{
+    std::lock_guard<std::mutex> lk(g_hmu);
+    for (Heap *h : g_heaps)
+        if (h->own.base == base) {
+            *len = h->own.len;
+            return true;
+        }
+    return false;
+}
+
+}  // namespace
+
+extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, int PE_size,
+                               long *pSync, char *report, size_t report_bytes)
+{
+    const char *where = "osgpu_preflight";
+    if (!pSync || PE_size < 1 || (report && !report_bytes)) {
+        set_err("%s: bad arguments", where);
+        return OSGPU_EINVAL;
+    }
+    Coll c = make_coll(where, PE_start, logPE_stride, PE_size, pSync);
+    const int me = c.index_of(c.me);
+    if (me < 0) {
+        set_err("%s: PE %d is not in the active set", where, c.me);
+        return OSGPU_EINVAL;
+    }
+    Heap *H = nullptr;
+    if (heap_base) {
+        std::lock_guard<std::mutex> lk(g_hmu);
+        for (Heap *h : g_heaps)
+            if (h->own.base == (char *) heap_base) H = h;
+    }
+    if (heap_base && (!H || H->members.size() != (size_t) PE_size)) {
+        set_err("%s: %p is not a heap of this active set made by osgpu_heap_create", where,
+                heap_base);
+        return OSGPU_EINVAL;  // the same on every member given the same arguments
+    }
+    // collective setups (same decision on every member)
+    StageSet *S = (PE_size > 1 && c.ops.getmem) ? stage_setup(c) : nullptr;
+    // flag areas exist only when every member is its own process
+    SyncSet *Y = (PE_size > 1 && c.ops.getmem) ? sync_setup(c) : nullptr;
+
+    // 1. my patterns
+    constexpr size_t B = 64;
+    unsigned long long w[B / 8];
+    auto put = [&](char *at, size_t bytes, int region, int chunk, int end) {
+        pattern(w, bytes / 8, c.me, region, chunk, end);
+        return hipMemcpy(at, w, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    bool wrote = true;
+    if (H) {
+        size_t off = 0;
+        for (size_t k = 0; k < H->own.len.size(); off += H->own.len[k], k++) {
+            wrote = put(H->own.base + off, B, 1, (int) k, 0) && wrote;
+            wrote = put(H->own.base + off + H->own.len[k] - B, B, 1, (int) k, 1) && wrote;
+        }
+    }
+    if (S) {
+        wrote = put(S->local, B, 2, 0, 0) && wrote;
+        wrote = put(S->local + 4 * S->slot - B, B, 2, 0, 1) && wrote;
+    }
+    if (Y) wrote = put((char *) (Y->local + 31), 8, 3, 0, 0) && wrote;
+    (void) hipDeviceSynchronize();
+    (void) hipGetLastError();
+    barrier(c);  // every member's patterns are in place
+
+    // 2. the peers' blocks through my mappings
+    std::vector<std::vector<Probe>> probes(PE_size);
+    for (int i = 0; i < PE_size; i++) {
+        if (i == me) continue;
+        if (H) {
+            std::vector<size_t> len;
+            bool have = false;
+            for (const Mapping &m : H->peers)
+                if (m.pe == c.pe_at(i)) {
+                    len = m.len;
+                    have = true;
+                }
+            if (!have) have = own_chunks(H->member_base[i], &len);  // a PE thread here
+            size_t off = 0;
+            for (size_t k = 0; have && k < len.size(); off += len[k], k++) {
+                probes[i].push_back({"heap", (int) k, 0, H->member_base[i] + off, B});
+                probes[i].push_back({"heap", (int) k, 1, H->member_base[i] + off + len[k] - B, B});
+            }
+        }
+        if (S) {
+            probes[i].push_back({"staging", 0, 0, S->region(i), B});
+            probes[i].push_back({"staging", 0, 1, S->region(i) + 4 * S->slot - B, B});
+        }
+        if (Y) probes[i].push_back({"flags", 0, 0, (const char *) (Y->peer[i] + 31), 8});
+    }
+    char *dtmp = nullptr;
+    const bool have_tmp = hipMalloc((void **) &dtmp, B) == hipSuccess;
+    (void) hipGetLastError();
+    hipStream_t st = thread_stream(where);
+    std::string rep = "{";
+    bool all = wrote;
+    int nprobes = 0, nbad = 0;
+    for (int i = 0; i < PE_size; i++) {
+        if (i == me) continue;
+        std::string bad;
+        for (const Probe &p : probes[i]) {
+            nprobes++;
+            unsigned long long want[B / 8], got[B / 8];
+            pattern(want, p.bytes / 8, c.pe_at(i), region_code(p.region), p.chunk, p.end);
+            const char *what = nullptr;
+            hipError_t e = hipMemcpy(got, p.addr, p.bytes, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) what = "host copy failed";
+            else if (memcmp(got, want, p.bytes)) what = "host copy read other data";
+            (void) hipGetLastError();
+            if (!what) {  // the copy kernel through the same mapping
+                osgpu::CopySeg seg = {p.addr, dtmp, p.bytes};
+                e = have_tmp ? osgpu::launch_copy(&seg, 1, st) : hipErrorOutOfMemory;
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e == hipSuccess) e = hipMemcpy(got, dtmp, p.bytes, hipMemcpyDeviceToHost);
+                if (e != hipSuccess) what = "copy kernel failed";
+                else if (memcmp(got, want, p.bytes)) what = "copy kernel read other data";
+                (void) hipGetLastError();
+            }
+            if (what) {
+                nbad++;
+                char b[160];
+                snprintf(b, sizeof(b), "%s%s %s%d %s: %s", bad.empty() ? "" : "; ", p.region,
+                         strcmp(p.region, "heap") ? "" : "chunk ",
+                         strcmp(p.region, "heap") ? 0 : p.chunk, p.end ? "high" : "low", what);
+                bad += b;
+            }
+        }
+        char b[96];
+        int nheap = 0;
+        for (const Probe &p : probes[i]) nheap += !strcmp(p.region, "heap") && p.end == 0;
+        snprintf(b, sizeof(b), "%s\"%d\": {\"chunks\": %d, \"staging\": %s, \"flags\": %s, ",
+                 rep.size() > 1 ? ", " : "", c.pe_at(i), nheap, S ? "true" : "false",
+                 Y ? "true" : "false");
+        rep += b;
+        rep += bad.empty() ? "\"status\": \"ok\"}" : "\"status\": \"" + bad + "\"}";
+        all = all && bad.empty();
+    }
+    rep += "}";
+    if (have_tmp) (void) hipFree(dtmp);
+    barrier(c);  // nobody reuses the regions before every member has read them
+    DBG("%s PE %d: %d probes, %d bad", where, c.me, nprobes, nbad);
+    if (report) {
+        if (rep.size() + 1 > report_bytes) {
+            set_err("%s: the report needs %zu bytes", where, rep.size() + 1);
+            snprintf(report, report_bytes, "%s", "{}");
+            return OSGPU_EINVAL;
+        }
+        memcpy(report, rep.c_str(), rep.size() + 1);
+    }
+    if (!wrote) set_err("%s: writing this PE's patterns failed", where);
+    else if (!all) set_err("%s: %d of %d probes failed", where, nbad, nprobes);
+    return all ? OSGPU_OK : OSGPU_EPEER;
 }

@@ -112,6 +112,9 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         // lane, not P*16 B per round trip.  G = U up to 4 inputs; above,
         // OSGPU_TEAM_G8 (all 4*P at once spills the 8-input complex sum)
         constexpr int G = P <= 4 ? U : OSGPU_TEAM_G8;
+        // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
+        // round reads and writes past the tile (and past nvec)
+        static_assert(G >= 1 && G <= U && U % G == 0, "OSGPU_TEAM_G8 must divide OSGPU_TEAM_U8");
 #pragma unroll
         for (int g = 0; g < U; g += G) {
             TVec<T> in[G][P];

@@ -114,6 +114,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_heap_translate.argtypes = [vp, i, i]
     L.osgpu_heap_create.argtypes = [sz, i, i, i, vp, ctypes.POINTER(vp)]
     L.osgpu_heap_destroy.argtypes = [vp]
+    L.osgpu_preflight.argtypes = [vp, i, i, i, vp, ctypes.c_char_p, sz]
     L.osgpu_heap_translate.restype = vp
     L.osgpu_ipc_get_handle.argtypes = [vp, vp]
     L.osgpu_ipc_open.argtypes = [vp]
@@ -210,6 +211,21 @@ def heap_create(nbytes: int, PE_start: int, logPE_stride: int, PE_size: int, psy
     if rc != 0:
         raise RuntimeError(f"osgpu_heap_create = {rc}: {L.osgpu_last_error().decode()}")
     return base.value
+
+
+def preflight(heap_base, PE_start: int, logPE_stride: int, PE_size: int, psync: int):
+    """osgpu_preflight (collective): (status code, per-peer report dict)."""
+    import json
+    L = load()
+    buf = ctypes.create_string_buffer(1 << 16)
+    rc = L.osgpu_preflight(heap_base, PE_start, logPE_stride, PE_size, psync, buf, len(buf))
+    try:
+        rep = json.loads(buf.value.decode() or "{}")
+    except ValueError:
+        rep = {"unparsed": buf.value.decode()[:400]}
+    if rc != 0:
+        rep["error"] = L.osgpu_last_error().decode()
+    return rc, rep
 
 
 def last_path() -> str:

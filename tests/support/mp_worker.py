@@ -151,25 +151,31 @@ def finalize_cycle_mode(L, PES, rank, world, cycles=4):
 
 
 def heap_leak_mode(L, PES, rank, world):
-    """(probe, not a test) create / destroy heaps of MP_LEAK_GIB GiB per PE
-    MP_LEAK_CYCLES times: if destroyed heaps kept their HBM, the creates
-    would fail once the cycles add up to more than the GPU holds."""
+    """create / destroy heaps of MP_LEAK_GIB GiB per PE (a comma list is
+    cycled: "16,8,16,4") MP_LEAK_CYCLES times, a reduction at the far end of
+    each heap checked against the oracle.  Destroyed heaps that another
+    process imported keep their HBM on this ROCm; heap.cpp's pool hands one
+    back (as a prefix) to every later create of the same member set up to
+    its size, so the cycles must never run out of HBM.  Then a create larger
+    than the device fails with OSGPU_ENOMEM on every member, at once."""
     import torch
     torch.cuda.set_device(0)
     PES.pes_barrier.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
     import oracle as O
-    gib = int(os.environ.get("MP_LEAK_GIB", "16"))
+    gibs = [int(x) for x in os.environ.get("MP_LEAK_GIB", "16").split(",")]
     cycles = int(os.environ.get("MP_LEAK_CYCLES", "20"))
     wrk = (ctypes.c_byte * 4096)()
     rsync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 4096
-    done, bases, bad = 0, [], 0
+    done, bases, bad, free_gib = 0, [], 0, []
     for k in range(cycles):
+        gib = gibs[k % len(gibs)]
         bp = ctypes.c_void_p()
         rc = L.osgpu_heap_create(gib << 30, 0, 0, world, psync, ctypes.byref(bp))
         if rc != 0:
             return {"leak_cycles_done": done, "leak_fail": L.osgpu_last_error().decode(),
-                    "leak_gib": gib, "leak_bases": bases, "leak_bad": bad}
+                    "leak_gib": gibs, "leak_bases": bases, "leak_bad": bad,
+                    "leak_free_gib": free_gib}
         base = bp.value
         bases.append(hex(base))
         # a reduction at the far end of the heap
@@ -187,14 +193,107 @@ def heap_leak_mode(L, PES, rank, world):
         osgpu.copy([out_t.data_ptr()], [base + off + n * 8], [n * 8])
         torch.cuda.synchronize()
         bad += int(not np.array_equal(out_t.cpu().numpy(), want))
+        # the registered size is the requested one: beyond it is not symmetric
+        past = L.osgpu_heap_translate(ctypes.c_void_p(base + (gib << 30) + 4096), rank,
+                                      (rank + 1) % world)
+        bad += int(past is not None)
+        del stage, out_t
         PES.pes_barrier(0, 0, world, None)
         assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
         PES.pes_barrier(0, 0, world, None)
         done += 1
-        print(f"heapleak rank {rank} cycle {k} ok, free {torch.cuda.mem_get_info()[0] >> 30} GiB",
+        free_gib.append(torch.cuda.mem_get_info()[0] / (1 << 30))
+        print(f"heapleak rank {rank} cycle {k} ({gib} GiB) ok, free {free_gib[-1]:.1f} GiB",
               flush=True)
-    return {"leak_cycles_done": done, "leak_fail": None, "leak_gib": gib, "leak_bases": bases,
-            "leak_bad": bad}
+    # more than the device holds: OSGPU_ENOMEM (-6) on every member, quickly
+    t0 = time.time()
+    bp = ctypes.c_void_p()
+    rc = L.osgpu_heap_create(1 << 50, 0, 0, world, psync, ctypes.byref(bp))
+    enomem = {"rc": rc, "error": L.osgpu_last_error().decode(), "seconds": time.time() - t0}
+    return {"leak_cycles_done": done, "leak_fail": None, "leak_gib": gibs, "leak_bases": bases,
+            "leak_bad": bad, "leak_free_gib": free_gib, "enomem": enomem}
+
+
+def preflight_mode(L, PES, rank, world):
+    """osgpu_preflight over a 3-chunk heap (OSGPU_HEAP_CHUNK_BYTES = 64 MiB),
+    the STAGED staging areas and the device-barrier flag areas: every probe
+    of every peer passes; then a team reduction on the same heap is
+    bit-exact (the probes' patterns do not disturb later use)."""
+    import torch
+    import oracle as O
+    torch.cuda.set_device(0)
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    bp = ctypes.c_void_p()
+    assert L.osgpu_heap_create(3 * (64 << 20), 0, 0, world, psync, ctypes.byref(bp)) == 0, \
+        L.osgpu_last_error().decode()
+    base = bp.value
+    rc, rep = osgpu.preflight(base, 0, 0, world, psync)
+    rc_none, rep_none = osgpu.preflight(None, 0, 0, world, psync)   # staging + flags only
+    assert not any(ctypes.string_at(psync, 512)), "pSync not reset"
+    n = 1 << 20
+    srcs = [O.gen_input("double", n, O.pe_seed(0x9F, r), "wide") for r in range(world)]
+    want = O.value_bytes(O.to_all("double", "sum", srcs)[rank]).reshape(-1)
+    stage = torch.from_numpy(np.ascontiguousarray(srcs[rank]).view(np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    off = (64 << 20) - n * 4            # straddles chunks 0 and 1
+    osgpu.copy([base + off], [stage.data_ptr()], [n * 8])
+    torch.cuda.synchronize()
+    dist.barrier()
+    wrk = (ctypes.c_byte * 4096)()
+    L.shmem_double_sum_to_all(base + off + n * 8, base + off, n, 0, 0, world, wrk,
+                              PES.pes_heap(rank) + PES.pes_heap_bytes() - 4096)
+    out_t = torch.empty(n * 8, dtype=torch.uint8, device="cuda:0")
+    osgpu.copy([out_t.data_ptr()], [base + off + n * 8], [n * 8])
+    torch.cuda.synchronize()
+    exact = bool(np.array_equal(out_t.cpu().numpy(), want))
+    ran = osgpu.last_path()
+    dist.barrier()
+    assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
+    return {"preflight_rc": rc, "preflight": rep, "preflight_none_rc": rc_none,
+            "preflight_none": rep_none, "after_exact": exact, "after_path": ran}
+
+
+def mixed_topology_mode(L, rank, world):
+    """2 processes x 2 PE threads (4 PEs): osgpu_heap_create must refuse the
+    topology on every member (OSGPU_EINVAL, a message naming it) instead of
+    importing each remote heap once per thread into ranges only that
+    thread's device may access (heap.cpp)."""
+    import threading
+    import torch
+    from support import peshm
+    torch.cuda.set_device(0)
+    P = peshm.load()
+    npes, hb = 2 * world, 1 << 20
+    name = f"/osgpu_pes_{os.environ.get('MASTER_PORT', '0')}mx".encode()
+    if rank == 0:
+        P.pes_unlink(name)
+        assert P.pes_init(name, 2 * rank, npes, hb, 1) == 0
+    dist.barrier()
+    if rank != 0:
+        assert P.pes_init(name, 2 * rank, npes, hb, 0) == 0
+    dist.barrier()
+    if rank == 0:
+        P.pes_unlink(name)
+    assert L.osgpu_set_pe_ops(P.pes_ops()) == 0
+    out = {}
+
+    def pe_thread(pe):
+        P.pes_set_thread_pe(pe)
+        torch.cuda.set_device(0)
+        bp = ctypes.c_void_p()
+        rc = L.osgpu_heap_create(64 << 20, 0, 0, npes, P.pes_heap(pe) + hb - 8192,
+                                 ctypes.byref(bp))
+        out[str(pe)] = {"rc": rc, "error": L.osgpu_last_error().decode()}
+        if rc == 0:
+            L.osgpu_heap_destroy(bp)
+
+    th = [threading.Thread(target=pe_thread, args=(2 * rank + t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dist.barrier()
+    return {"mixed": out}
 
 
 def heap_cycle_mode(L, PES, rank, world, cycles=6):
@@ -999,7 +1098,7 @@ def main():
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
             "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle", "heapleak",
-            "fuzz"):
+            "fuzz", "preflight"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -1062,6 +1161,10 @@ def main():
         res.update(heap_cycle_mode(L, PES, rank, world))
     if mode == "heapleak":
         res.update(heap_leak_mode(L, PES, rank, world))
+    if mode == "preflight":
+        res.update(preflight_mode(L, PES, rank, world))
+    if mode == "mixedtopo":
+        res.update(mixed_topology_mode(L, rank, world))
     if mode == "finalizecycle":
         res.update(finalize_cycle_mode(L, PES, rank, world))
     if mode == "hostcoll":

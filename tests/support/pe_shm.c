@@ -11,6 +11,8 @@
  *   shmem_getmem                memcpy from the peer's slot of a shared host
  *                               heap at the same offset (XPMEM-style; the
  *                               base-offset translation of src/shmemc/comms.c:89-105)
+ * pes_set_thread_pe lets a thread act as another PE (jobs mixing PE threads
+ * and PE processes, to test that the library refuses them where it must).
  */
 #define _GNU_SOURCE
 #include <fcntl.h>
@@ -70,7 +72,10 @@ int pes_init(const char *name, int me, int npes, unsigned long long heap_bytes, 
 
 int pes_unlink(const char *name) { return shm_unlink(name); }
 
-int pes_my_pe(void) { return g_me; }
+/* several PEs per process (threads): a thread may take another PE's rank */
+static __thread int t_me = -1;
+void pes_set_thread_pe(int pe) { t_me = pe; }
+int pes_my_pe(void) { return t_me >= 0 ? t_me : g_me; }
 int pes_n_pes(void) { return g_npes; }
 
 void *pes_heap(int pe) { return g_heap + (size_t) pe * g_hdr->heap_bytes; }
@@ -120,7 +125,7 @@ void pes_barrier(int PE_start, int logPE_stride, int PE_size, long *pSync)
 
 void pes_getmem(void *dest, const void *src, size_t n, int pe)
 {
-    const char *s = (const char *) src, *mine = (const char *) pes_heap(g_me);
+    const char *s = (const char *) src, *mine = (const char *) pes_heap(pes_my_pe());
     if (pe < 0 || pe >= g_npes || s < mine || s + n > mine + g_hdr->heap_bytes) {
         fprintf(stderr, "pe_shm: getmem of a non-symmetric address\n");
         abort();

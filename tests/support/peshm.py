@@ -29,6 +29,7 @@ def load():
     L.pes_heap.restype = ctypes.c_void_p
     L.pes_heap_bytes.restype = ctypes.c_ulonglong
     L.pes_ops.restype = ctypes.c_void_p
+    L.pes_set_thread_pe.argtypes = [ctypes.c_int]
     vp, i = ctypes.c_void_p, ctypes.c_int
     L.pes_time_to_all.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, i]
     L.pes_time_to_all.restype = ctypes.c_double

@@ -51,6 +51,49 @@ def test_completed_line_printed_once():
     assert len(lines) == 1 and "incomplete" not in json.loads(lines[0])
 
 
+def _spawn(*extra, ndev="0"):
+    env = dict(os.environ, BENCH_NDEV=ndev, BENCH_RANK_GRACE_S="5")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+              "GPU_MAX_HW_QUEUES"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                           "--dry-ranks", "--deadline", "60", *extra],
+                          capture_output=True, text=True, timeout=240, env=env)
+
+
+def test_spawn_without_torchrun_plumbs_every_rank():
+    """`python bench.py --gpus N` with no RANK: the parent starts N ranks
+    itself (no torchrun), each with the torch.distributed.run environment;
+    they meet over gloo at MASTER_ADDR:MASTER_PORT and rank 0's line is
+    relayed once.  3 ranks on 1 GPU: each gets the 16-queue share."""
+    r = _spawn(ndev="1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["dry"] and d["n_gpus"] == 3
+    ranks = d["ranks"]
+    assert [x["RANK"] for x in ranks] == ["0", "1", "2"]
+    assert [x["LOCAL_RANK"] for x in ranks] == ["0", "1", "2"]
+    assert {x["WORLD_SIZE"] for x in ranks} == {"3"}
+    assert {x["MASTER_ADDR"] for x in ranks} == {"127.0.0.1"}
+    assert {x["GPU_MAX_HW_QUEUES"] for x in ranks} == {"5"}      # 16 // 3
+    assert len({x["pid"] for x in ranks}) == 3
+
+
+def test_spawn_no_queue_cap_with_a_gpu_per_rank():
+    r = _spawn(ndev="8")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert {x["GPU_MAX_HW_QUEUES"] for x in d["ranks"]} == {None}
+
+
+def test_spawn_fails_loudly_when_a_rank_fails():
+    r = _spawn("--dry-fail-rank", "2")
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert "rank exit codes" in r.stderr
+
+
 def test_defaults_single_gpu_within_minutes():
     sys.path.insert(0, ROOT)
     import bench

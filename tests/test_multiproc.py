@@ -363,23 +363,72 @@ def test_finalize_cycles_processes(tmp_path):
 
 @pytest.mark.gpu
 def test_heap_reuse_processes(tmp_path, monkeypatch):
-    """Twelve rounds of a 32 GiB heap made and destroyed by 2 processes:
-    768 GiB in all, which the GPU only holds because a destroyed heap with
-    imported chunks is kept and handed back to the next create of the same
-    member set and size (heap.cpp g_pool) -- same base every round, and a
-    reduction at the heap's far end bit-exact each time."""
+    """Twelve rounds of heaps of 16, 8, 16 and 4 GiB per PE made and
+    destroyed by 2 processes (144 GiB per PE in all).  A destroyed heap with
+    imported chunks keeps its HBM on this ROCm; heap.cpp's pool hands it
+    back, as a prefix of its range, to every later create of the same member
+    set up to its size -- same base every round, free HBM flat after the
+    first, a reduction at each heap's far end bit-exact against the oracle,
+    nothing registered past the requested size.  Then a create larger than
+    the device fails with OSGPU_ENOMEM (-6) on every member within seconds."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if torch.cuda.mem_get_info()[1] < (100 << 30):
         pytest.skip("needs a GPU of at least 100 GiB")
-    monkeypatch.setenv("MP_LEAK_GIB", "32")
+    monkeypatch.setenv("MP_LEAK_GIB", "16,8,16,4")
     monkeypatch.setenv("MP_LEAK_CYCLES", "12")
     res = launch("heapleak", 2, tmp_path, timeout=400)
     for r in res:
         assert r["leak_fail"] is None and r["leak_cycles_done"] == 12, r
         assert r["leak_bad"] == 0, r
         assert len(set(r["leak_bases"])) == 1, r
+        assert min(r["leak_free_gib"]) > r["leak_free_gib"][0] - 1.0, r["leak_free_gib"]
+        e = r["enomem"]
+        assert e["rc"] == -6 and e["seconds"] < 10, e
+        assert "out of device memory" in e["error"], e
+
+
+@pytest.mark.gpu
+def test_preflight_processes(tmp_path, monkeypatch):
+    """osgpu_preflight with 3 processes on cuda:0 over a heap of three
+    64-MiB chunks: every chunk end, staging area and flag word of every peer
+    reads back its owner's pattern through this process's mapping (host copy
+    and copy kernel); a reduction on the same heap afterwards is bit-exact."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("OSGPU_HEAP_CHUNK_BYTES", str(64 << 20))
+    world = 3
+    res = launch("preflight", world, tmp_path, timeout=300)
+    for r in range(world):
+        x = res[r]
+        assert x["preflight_rc"] == 0, x["preflight"]
+        peers = sorted(x["preflight"])
+        assert peers == sorted(str(p) for p in range(world) if p != r), x["preflight"]
+        for p in peers:
+            e = x["preflight"][p]
+            assert e == {"chunks": 3, "staging": True, "flags": True, "status": "ok"}, (r, p, e)
+            f = x["preflight_none"][p]
+            assert f["chunks"] == 0 and f["staging"] and f["status"] == "ok", (r, p, f)
+        assert x["after_exact"] and x["after_path"] == "team", x
+
+
+@pytest.mark.gpu
+def test_heap_refuses_mixed_topology(tmp_path):
+    """2 processes x 2 PE threads: osgpu_heap_create refuses the topology
+    on all 4 PEs (OSGPU_EINVAL with a message) -- never per-thread imports
+    registered process-wide (the last writer would win)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = launch("mixedtopo", 2, tmp_path, timeout=200)
+    got = {}
+    for r in res:
+        got.update(r["mixed"])
+    assert sorted(got) == ["0", "1", "2", "3"], got
+    for pe, x in got.items():
+        assert x["rc"] == -1 and "unsupported topology" in x["error"], (pe, x)
 
 
 @pytest.mark.gpu
