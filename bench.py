@@ -301,26 +301,29 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
     return span_per_launch(torch, st, launch, reps), a, b, out
 
 
-def team_kernel_rate(L, torch, n, reps):
+def team_kernel_rate(L, torch, n, reps, P=2):
     """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
-    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,2>
+    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>
     through the C ABI (osgpu_team_combine), one launch over all n elements --
-    the work the two PEs' shard launches of a 2-PE call do together: reads
-    both sources once, writes both targets (PE 0: x0+x1, PE 1: x1+x0).
-    Algorithmic bytes 4*n*8 per launch.  HIP events on the launch stream."""
+    the work the P PEs' shard launches of a P-PE call do together: reads
+    every source once, writes every target (PE q: x_q + the others in
+    ascending order).  Algorithmic bytes 2*P*n*8 per launch.  HIP events on
+    the launch stream.  Beside it the same-mix ceiling: the copy kernel
+    (csrc/copy.hip) moving P ranges of n*8 bytes in one launch -- P read
+    and P write streams over the same bytes, nothing folded."""
     dev = torch.device("cuda:0")
-    a = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0)
-    b = torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0)
-    o0 = torch.empty(n, dtype=torch.float64, device=dev)
-    o1 = torch.empty(n, dtype=torch.float64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(11)
+    srcs_t = [torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0, generator=g)
+              for _ in range(P)]
+    dsts_t = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(P)]
     st = torch.cuda.Stream(device=dev)
-    srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
-    dsts = (ctypes.c_void_p * 2)(o0.data_ptr(), o1.data_ptr())
+    srcs = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs_t])
+    dsts = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts_t])
     sp = ctypes.c_void_p(st.cuda_stream)
     torch.cuda.synchronize()
 
     def launch():
-        if L.osgpu_team_combine(5, 0, 2, dsts, srcs, n, sp) != 0:
+        if L.osgpu_team_combine(5, 0, P, dsts, srcs, n, sp) != 0:
             raise RuntimeError(L.osgpu_last_error().decode())
 
     for _ in range(3):
@@ -334,20 +337,45 @@ def team_kernel_rate(L, torch, n, reps):
         e1.record(st)
     torch.cuda.synchronize()
     ks = [e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev]
-    exact = bool(torch.equal(o0, a + b) and torch.equal(o1, b + a))
-    B = 4 * n * 8
-    tr = load_traffic("team_vec_kernel<double, 0, 2, true>", n)
+    # bit-exact: member q's fold order is q first, then ascending skipping q
+    exact = True
+    idx = torch.randint(0, n, (1 << 16,), device=dev, generator=g)
+    for q in range(P):
+        acc = srcs_t[q][idx].clone()
+        for j in range(P):
+            if j != q:
+                acc = acc + srcs_t[j][idx]
+        exact = exact and bool(torch.equal(dsts_t[q][idx], acc))
+    # the same-mix ceiling: copy kernel, P ranges src_p -> dst_p in one launch
+    S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs_t])
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts_t])
+    N = (ctypes.c_size_t * P)(*([n * 8] * P))
+
+    def copy():
+        assert L.osgpu_copy(D, S, N, P, sp) == 0
+    for _ in range(3):
+        copy()
+    cavg = span_per_launch(torch, st, copy, reps)
+    B = 2 * P * n * 8
+    kern = f"team_vec_kernel<double, 0, {P}, true>"
+    tr = load_traffic(kern, n if P == 2 else None)
+    frac = B / kavg / 1e9 / HBM_PEAK_GBS
+    cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
-           "traffic": tr.get("bytes_per_launch") if tr else None,
-           "kernel": "osgpu::team_vec_kernel<double, SUM, 2, ordered>",
+           "frac": frac, "traffic": tr.get("bytes_per_launch") if tr else None,
+           "kernel": f"osgpu::team_vec_kernel<double, SUM, {P}, ordered>",
+           "members": P, "nreduce": n,
            "kernel_avg_us": kavg * 1e6,
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
            "kernel_min_us_per_launch_events": min(ks) * 1e6,
-           "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact": exact,
-           "note": "one launch over all nreduce elements = both PEs' shard launches of a 2-PE "
-                   "call; 2 reads + 2 writes of 8 B per element"}
-    del a, b, o0, o1
+           "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact_sample": exact,
+           "copy_ceiling_same_mix": {"kernel": "copy_vec_kernel", "ranges": P,
+                                     "bytes_per_range": n * 8, "us": cavg * 1e6,
+                                     "frac_of_8TBs": cfrac},
+           "frac_of_copy_ceiling": frac / cfrac,
+           "note": f"one launch over all nreduce elements = the {P} PEs' shard launches of a "
+                   f"{P}-PE call; {P} reads + {P} writes of 8 B per element"}
+    del srcs_t, dsts_t
     torch.cuda.empty_cache()
     return out
 
@@ -573,11 +601,20 @@ def bench_single(args):
     }
     if "frac_of_8TBs" in ceil64:
         res["roofline"]["frac_of_copy_ceiling"] = res["roofline"]["frac"] / ceil64["frac_of_8TBs"]
-    # the kernel the API dispatches (TEAM path), under the same roofline
+    # the kernel the API dispatches (TEAM path), under the same roofline, for
+    # 2, 4 and 8 members (config 4's 8 PEs on one GPU run it at P = 8), each
+    # beside the copy kernel moving the same P read + P write streams
     try:
         res["roofline_team"] = team_kernel_rate(L, torch, n, args.steps)
     except Exception as e:  # report, never hide
         res["roofline_team"] = {"error": repr(e)}
+    res["roofline_team_by_members"] = {}
+    for P in ((4, 8) if not args.no_extra else ()):
+        try:
+            res["roofline_team_by_members"][str(P)] = team_kernel_rate(
+                L, torch, n, min(args.steps, 20), P)
+        except Exception as e:  # report, never hide
+            res["roofline_team_by_members"][str(P)] = {"error": repr(e)}
     if not args.no_api:
         try:
             res["api"] = api_call_time(n)
@@ -1313,6 +1350,9 @@ def bench_multi(args):
                                            "remote writes, per link per direction")
                 if ndev >= world:
                     rf["frac_of_measured_peak"] = rf["achieved"] / ((world - 1) * link)
+                else:   # ranks share a GPU: the probe moved HBM, not a link
+                    rf["peak_measured_link_GBs"] = None
+                    rf["peak_measured_how"] += "; not measured: ranks share a GPU in this run"
             _log(rank, "xgmi probe done")
         except Exception as e:
             res["xgmi_probe"] = {"error": repr(e)[:300]}
