@@ -959,8 +959,9 @@ def bench_multi(args):
     # torch.distributed.run a child process counts them)
     ndev = device_count_without_hip()
     cap = hw_queue_cap(world, ndev)
-    if cap is not None:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", cap)
+    if cap is not None:     # the box may export HIP's default (4): lower it, never raise it
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(cap), int(os.environ.get(
+            "GPU_MAX_HW_QUEUES", cap))))
     import torch
     import torch.distributed as dist
     import osgpu
@@ -1437,8 +1438,9 @@ def launch_ranks(args, argv):
                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                 BENCH_NDEV=str(ndev), PYTHONUNBUFFERED="1")
     cap = hw_queue_cap(world, ndev)
-    if cap is not None and "GPU_MAX_HW_QUEUES" not in os.environ:
-        env0["GPU_MAX_HW_QUEUES"] = cap
+    if cap is not None:     # the box may export HIP's default (4): lower it, never raise it
+        env0["GPU_MAX_HW_QUEUES"] = str(min(int(cap), int(os.environ.get("GPU_MAX_HW_QUEUES",
+                                                                          cap))))
     procs = []
     for r in range(world):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))

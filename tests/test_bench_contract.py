@@ -51,12 +51,14 @@ def test_completed_line_printed_once():
     assert len(lines) == 1 and "incomplete" not in json.loads(lines[0])
 
 
-def _spawn(*extra, ndev="0"):
+def _spawn(*extra, ndev="0", world=3, hwq=None):
     env = dict(os.environ, BENCH_NDEV=ndev, BENCH_RANK_GRACE_S="5")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
               "GPU_MAX_HW_QUEUES"):
         env.pop(k, None)
-    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+    if hwq is not None:
+        env["GPU_MAX_HW_QUEUES"] = hwq
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world),
                            "--dry-ranks", "--deadline", "60", *extra],
                           capture_output=True, text=True, timeout=240, env=env)
 
@@ -79,6 +81,15 @@ def test_spawn_without_torchrun_plumbs_every_rank():
     assert {x["MASTER_ADDR"] for x in ranks} == {"127.0.0.1"}
     assert {x["GPU_MAX_HW_QUEUES"] for x in ranks} == {"5"}      # 16 // 3
     assert len({x["pid"] for x in ranks}) == 3
+
+
+def test_spawn_lowers_an_exported_queue_count():
+    """The GPU box exports HIP's default GPU_MAX_HW_QUEUES=4: 6 ranks sharing
+    one GPU must still get 16 // 6 = 2 each (else 24 queues time-slice)."""
+    r = _spawn(ndev="1", world=6, hwq="4")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert {x["GPU_MAX_HW_QUEUES"] for x in d["ranks"]} == {"2"}
 
 
 def test_spawn_no_queue_cap_with_a_gpu_per_rank():

@@ -44,9 +44,10 @@ def launch(mode, world, tmp_path, timeout=600):
     # (HIP's default is four per process; more than 16 on the GPU and its
     # scheduler time-slices the queues in milliseconds, INTEGRATION.md,
     # profiles/r02_mp_latency_hwq.jsonl).  MP_HWQ=default keeps HIP's default.
-    if world > 4 and "GPU_MAX_HW_QUEUES" not in os.environ and \
-            os.environ.get("MP_HWQ") != "default":
-        extra["GPU_MAX_HW_QUEUES"] = str(max(1, 16 // world))
+    # (the box exports HIP's default, 4: lowered here, never raised)
+    if world > 4 and os.environ.get("MP_HWQ") != "default":
+        extra["GPU_MAX_HW_QUEUES"] = str(min(max(1, 16 // world),
+                                             int(os.environ.get("GPU_MAX_HW_QUEUES", "16"))))
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1",
