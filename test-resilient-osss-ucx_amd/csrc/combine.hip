@@ -63,16 +63,30 @@ __device__ __forceinline__ T fold_scalar(const Inputs<T, K> &in, size_t i)
     return acc;
 }
 
+// the branch-free fold (elem_ops.hpp Fast), redone with the exact one only
+// for a vector whose result holds a NaN part: no branch per element
 template <typename T, int OP, int K>
 __device__ __forceinline__ void fold_vec(Vec16<T> (&x)[K], Vec16<T> &out)
 {
     constexpr int W = 16 / sizeof(T);
+    using F = Fast<T, OP>;
+    bool bad = false;
 #pragma unroll
     for (int w = 0; w < W; w++) {
         T acc = x[0].e[w];
 #pragma unroll
-        for (int k = 1; k < K; k++) acc = Elem<T, OP>::f(acc, x[k].e[w]);
+        for (int k = 1; k < K; k++) acc = F::f(acc, x[k].e[w]);
         out.e[w] = acc;
+        bad = bad || F::bad(acc);
+    }
+    if (F::kChecked && __builtin_expect(bad, 0)) {
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            T acc = x[0].e[w];
+#pragma unroll
+            for (int k = 1; k < K; k++) acc = Elem<T, OP>::f(acc, x[k].e[w]);
+            out.e[w] = acc;
+        }
     }
 }
 

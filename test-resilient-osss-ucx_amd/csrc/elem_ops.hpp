@@ -194,4 +194,57 @@ template <> struct Elem<cfloat, OP_PROD> {
     __device__ __forceinline__ static cfloat f(cfloat a, cfloat b) { return cmul<cfloat, float>(a, b); }
 };
 
+// ------------------------------------------------------- branch-free folds
+// Fast<T, OP>::f is Elem<T, OP>::f without its NaN handling (the SSE rule,
+// the complex product's libgcc recovery): one instruction stream with no
+// branch per element, so a streaming kernel keeps every load in flight.
+// It differs from Elem::f only where that result has a NaN part, and a NaN
+// part, once there, stays through every later + and * of a fold (x + NaN,
+// x * NaN and both complex formulas give NaN in it).  So a fold whose FINAL
+// value has no NaN part (Fast::bad false) is bit-identical to the exact
+// fold; kernels test the final values of a tile and recompute the tile with
+// Elem::f only where some lane's is flagged.  Ops without NaN handling
+// (integers, min/max, which never produce a NaN of their own) are exact:
+// kChecked = false and the test compiles away.
+template <typename T, int OP> struct Fast {
+    static constexpr bool kChecked = false;
+    __device__ __forceinline__ static T f(T a, T b) { return Elem<T, OP>::f(a, b); }
+    __device__ __forceinline__ static bool bad(T) { return false; }
+};
+template <typename F, int OP> struct FastReal {
+    static constexpr bool kChecked = true;
+    __device__ __forceinline__ static F f(F a, F b) { return OP == OP_SUM ? a + b : a * b; }
+    __device__ __forceinline__ static bool bad(F r) { return r != r; }
+};
+template <> struct Fast<float, OP_SUM> : FastReal<float, OP_SUM> {};
+template <> struct Fast<float, OP_PROD> : FastReal<float, OP_PROD> {};
+template <> struct Fast<double, OP_SUM> : FastReal<double, OP_SUM> {};
+template <> struct Fast<double, OP_PROD> : FastReal<double, OP_PROD> {};
+template <> struct Fast<cdouble, OP_SUM> {
+    static constexpr bool kChecked = true;
+    __device__ __forceinline__ static cdouble f(cdouble a, cdouble b)
+    {
+        return cdouble{a.re + b.re, a.im + b.im};
+    }
+    __device__ __forceinline__ static bool bad(cdouble r) { return r.re != r.re || r.im != r.im; }
+};
+template <> struct Fast<cfloat, OP_SUM> {
+    static constexpr bool kChecked = true;
+    __device__ __forceinline__ static cfloat f(cfloat a, cfloat b)
+    {
+        return cfloat{a.re + b.re, b.im + a.im};  // the compiled order, as Elem
+    }
+    __device__ __forceinline__ static bool bad(cfloat r) { return r.re != r.re || r.im != r.im; }
+};
+template <typename C, typename F> struct FastCplxProd {
+    static constexpr bool kChecked = true;
+    __device__ __forceinline__ static C f(C p, C q)
+    {
+        return C{p.re * q.re - p.im * q.im, p.re * q.im + p.im * q.re};  // cmul's inline form
+    }
+    __device__ __forceinline__ static bool bad(C r) { return r.re != r.re || r.im != r.im; }
+};
+template <> struct Fast<cdouble, OP_PROD> : FastCplxProd<cdouble, double> {};
+template <> struct Fast<cfloat, OP_PROD> : FastCplxProd<cfloat, float> {};
+
 }  // namespace osgpu

@@ -42,17 +42,31 @@ struct TeamPtrs {
 constexpr int kTeamBlock = 256;
 
 // above 4 members: U vectors per input per lane, G of them in flight per
-// round.  U = G = 2 (16 vectors of 16 B in flight per lane at 8 members, one
-// round) beat U = 4 in two rounds of 2 by 1-3 % at P = 8, every type
-// (profiles/r02_team_variants.jsonl); the pull combine keeps OSGPU_U_K8
+// round.  With the branch-free folds (elem_ops.hpp Fast), U = 4 in two
+// rounds of G = 2 (16 vectors of 16 B in flight per lane at 8 members)
+// beats one round of U = G = 2 at P = 8 for every type: float 0.715 ->
+// 0.786, complexf 0.723 -> 0.790 of 8 TB/s, int / long +2 %, the rest equal
+// (every build loaded in one process, interleaved on the same arrays,
+// profiles/r03_team_variants_interleaved.jsonl); U = G = 4 spills the
+// 8-input complexf fold (0.45).  The pull combine keeps OSGPU_U_K8
 #ifndef OSGPU_TEAM_U8
-#define OSGPU_TEAM_U8 2
+#define OSGPU_TEAM_U8 4
 #endif
 #ifndef OSGPU_TEAM_G8
-#define OSGPU_TEAM_G8 OSGPU_TEAM_U8
+#define OSGPU_TEAM_G8 2
+#endif
+// vectors per input per lane for 2 and for 3-4 members (all loaded before
+// the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
+// (same interleaved A/B)
+#ifndef OSGPU_TEAM_U2
+#define OSGPU_TEAM_U2 OSGPU_U_K2
+#endif
+#ifndef OSGPU_TEAM_U4
+#define OSGPU_TEAM_U4 OSGPU_U_K4
 #endif
 
-template <typename T, int OP, int P, bool ORDERED>
+// E: Elem<T, OP> (exact) or Fast<T, OP> (branch-free, elem_ops.hpp)
+template <typename T, int OP, int P, bool ORDERED, typename E = Elem<T, OP>>
 __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
 {
     if (ORDERED) {
@@ -61,13 +75,13 @@ __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
             T acc = x[q];
 #pragma unroll
             for (int j = 0; j < P; j++)
-                if (j != q) acc = Elem<T, OP>::f(acc, x[j]);
+                if (j != q) acc = E::f(acc, x[j]);
             r[q] = acc;
         }
     } else {
         T acc = x[0];
 #pragma unroll
-        for (int j = 1; j < P; j++) acc = Elem<T, OP>::f(acc, x[j]);
+        for (int j = 1; j < P; j++) acc = E::f(acc, x[j]);
 #pragma unroll
         for (int q = 0; q < P; q++) r[q] = acc;
     }
@@ -79,7 +93,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                                                               int nedge)
 {
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_TEAM_U8);
+    constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -90,17 +104,36 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
     const size_t t0 = (size_t) blockIdx.x * (kTeamBlock * U) + threadIdx.x;
-    // fold one vector of every input into one vector of every output
+    // fold one vector of every input into one vector of every output: the
+    // branch-free fold first, the exact one only for a vector whose results
+    // hold a NaN part (rare; elem_ops.hpp Fast) -- no branch per element, so
+    // the tile's loads stay in flight ahead of the folds
+    using F = Fast<T, OP>;
     auto fold_store = [&](TVec<T> (&in)[P], size_t j) {
         TVec<T> out[P];
+        bool bad = false;
 #pragma unroll
         for (int w = 0; w < W; w++) {
             T x[P], r[P];
 #pragma unroll
             for (int p = 0; p < P; p++) x[p] = in[p].e[w];
-            team_fold<T, OP, P, ORDERED>(x, r);
+            team_fold<T, OP, P, ORDERED, F>(x, r);
 #pragma unroll
-            for (int p = 0; p < P; p++) out[p].e[w] = r[p];
+            for (int p = 0; p < P; p++) {
+                out[p].e[w] = r[p];
+                bad = bad || F::bad(r[p]);
+            }
+        }
+        if (F::kChecked && __builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                T x[P], r[P];
+#pragma unroll
+                for (int p = 0; p < P; p++) x[p] = in[p].e[w];
+                team_fold<T, OP, P, ORDERED>(x, r);
+#pragma unroll
+                for (int p = 0; p < P; p++) out[p].e[w] = r[p];
+            }
         }
 #pragma unroll
         for (int p = 0; p < P; p++)
@@ -181,7 +214,7 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_U_K2 : (P <= 4 ? OSGPU_U_K4 : OSGPU_TEAM_U8);
+    constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
     size_t head = phase ? (16 - phase) / sizeof(T) : 0;
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;

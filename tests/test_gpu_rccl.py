@@ -103,3 +103,33 @@ def test_rccl_collectives(rccl_team):
     tm.run_coll("broadcast", 64, toff, 0, n, PE_root=0)
     assert tm.last_coll_paths[0] == "rccl"
     assert (tm.read(0, toff, n * 8) == 0x5A).all()
+
+
+@pytest.mark.parametrize("t,op,dt", [("int", "sum", "int32"), ("long", "prod", "int64"),
+                                     ("int", "min", "int32"), ("long", "max", "int64")])
+def test_auto_path_sends_integer_arrays_outside_the_heaps_to_rccl(rccl_team, t, op, dt):
+    """OSGPU_PATH_AUTO with a heap registered: arrays OUTSIDE every heap of
+    an integer (type, op) go to ncclAllReduce (order-independent, so
+    bit-exact), the dispatch bench.py's N>1 line checks against the oracle
+    across GPUs (`rccl_integer_auto`).  Here (1 rank) the result is the
+    source, wrap-around values included."""
+    import torch
+    tm = rccl_team
+    tm.activate()
+    L = tm.lib
+    L.osgpu_set_path(osgpu.PATH_AUTO)
+    try:
+        n = 100_003
+        tdt = getattr(torch, dt)
+        info = torch.iinfo(tdt)
+        src = torch.randint(info.min, info.max, (n,), dtype=tdt, device="cuda",
+                            generator=torch.Generator(device="cuda").manual_seed(9))
+        dst = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        wrk = (ctypes.c_long * 64)()
+        tm.pet.pet_set_me(0)
+        osgpu.to_all(t, op)(dst.data_ptr(), src.data_ptr(), n, 0, 0, 1, wrk, tm.psync_ptr(0))
+        assert osgpu.last_path() == "rccl"
+        assert torch.equal(dst, src)
+    finally:
+        L.osgpu_set_path(osgpu.PATH_RCCL)

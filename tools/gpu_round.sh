@@ -42,6 +42,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     multi_self) step multi_self 420 python bench.py --gpus 2 --steps 5 --warmup 2 --deadline 360 ;;
     multi_self4) step multi_self4 420 python bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((16<<20)) --c4-nreduce $((64<<20)) --c5-nreduce $((16<<20)) --deadline 360 ;;
     multi8) step multi8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
+    teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
+    tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
     multi8_self) step multi8_self 900 python bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     multi4_s) step multi4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 200 ;;

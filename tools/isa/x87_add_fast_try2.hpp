@@ -1,0 +1,479 @@
+// x87.hpp -- bit-exact x87 80-bit extended arithmetic (host + device).
+// Used by longdouble.hip on the GPU; the identical code is compiled for the
+// host only by tests/support (to check it against the reference's own x87
+// ops on millions of inputs before it runs on an MI355X).
+// See longdouble.hip for the semantics.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef OSGPU_HD
+#define OSGPU_HD __host__ __device__
+#endif
+
+namespace osgpu {
+namespace x87 {
+
+typedef unsigned __int128 u128;
+
+struct X80 {
+    uint64_t m;   // significand, bit 63 = explicit integer bit J
+    uint32_t se;  // bit 15 sign, bits 0..14 biased exponent
+};
+
+enum Cls { C_ZERO, C_FIN, C_INF, C_QNAN, C_SNAN, C_BAD };
+
+constexpr int kBias = 16383;
+constexpr uint32_t kEmax = 0x7fff;
+
+OSGPU_HD inline X80 defnan() { return X80{0xC000000000000000ull, 0xFFFFu}; }
+
+OSGPU_HD inline Cls classify(X80 x)
+{
+    const uint32_t e = x.se & kEmax;
+    const bool j = (x.m >> 63) != 0;
+    if (e == kEmax) {
+        if (!j) return C_BAD;                      // pseudo-infinity / pseudo-NaN
+        if ((x.m << 1) == 0) return C_INF;
+        return ((x.m >> 62) & 1) ? C_QNAN : C_SNAN;
+    }
+    if (e == 0) return x.m == 0 ? C_ZERO : C_FIN;    // denormal or pseudo-denormal
+    return j ? C_FIN : C_BAD;                        // unnormal is unsupported
+}
+
+OSGPU_HD inline bool is_nan(Cls c) { return c == C_QNAN || c == C_SNAN; }
+
+OSGPU_HD inline int clz128(u128 v)
+{
+    const uint64_t hi = (uint64_t) (v >> 64), lo = (uint64_t) v;
+    return hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);
+}
+
+// NaN propagation with at least one NaN operand and no unsupported one
+OSGPU_HD inline X80 nan_pick(X80 a, Cls ca, X80 b, Cls cb)
+{
+    X80 r;
+    if (is_nan(ca) && is_nan(cb)) {
+        if (a.m > b.m) r = a;
+        else if (b.m > a.m) r = b;
+        else r = X80{a.m, (a.se & b.se)};        // tie: positive if either is
+    } else {
+        r = is_nan(ca) ? a : b;
+    }
+    r.m |= 1ull << 62;                           // quiet
+    return r;
+}
+
+// Round a value sign * S * 2^(E - bias - 127), S normalised with bit 127 set
+// (or S == 0), to x87 extended and encode it.
+OSGPU_HD inline X80 round_pack(uint32_t sign, int E, u128 S)
+{
+    if (S == 0) return X80{0, sign << 15};
+    if (E < 1) {                                 // gradual underflow
+        const int sh = 1 - E;
+        if (sh >= 128) {
+            S = 1;                               // sticky only
+        } else {
+            const bool sticky = (S << (128 - sh)) != 0;
+            S = (S >> sh) | (u128) (sticky ? 1 : 0);
+        }
+        E = 1;
+    }
+    uint64_t hi = (uint64_t) (S >> 64);
+    const uint64_t lo = (uint64_t) S;
+    const bool half = (lo >> 63) != 0;
+    const bool rest = (lo << 1) != 0;
+    if (half && (rest || (hi & 1))) {
+        hi += 1;
+        if (hi == 0) {                           // carried out of 64 bits
+            hi = 1ull << 63;
+            E += 1;
+        }
+    }
+    if (E >= (int) kEmax) return X80{1ull << 63, (sign << 15) | kEmax};  // overflow -> inf
+    const uint32_t e = (hi >> 63) ? (uint32_t) E : 0u;                    // denormal if J=0
+    return X80{hi, (sign << 15) | e};
+}
+
+// The general add: every encoding, exact 128-bit intermediate, one RNE
+// rounding (below).
+OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b);
+
+// Unpacked operand of the fast add: significand, biased exponent and sign
+// in their own registers, so a fold that feeds one add's result to the next
+// (and reuses each input P-1 times) does not re-extract them every time.
+struct XU {
+    uint64_t m;
+    uint32_t e;  // biased exponent, 0..0x7fff
+    uint32_t s;  // sign, 0 or 1
+};
+
+OSGPU_HD inline XU unpack_u(X80 x) { return XU{x.m, x.se & kEmax, (x.se >> 15) & 1}; }
+OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s << 15) | x.e}; }
+
+OSGPU_HD inline bool normal_u(XU x) { return x.e - 1u < kEmax - 1u && (x.m >> 63); }
+
+// add of two NORMAL operands (0 < biased exponent < 0x7fff, J set; the
+// caller checks), straight-line: the data-dependent choices (swap, add or
+// subtract, renormalising shift, round up) are selects, so the lanes of a
+// wave -- and several independent folds of one lane -- run one instruction
+// stream.  Returns false where it does not apply: exponent gaps of 64 and 65,
+// cancellation into the low half (exact zero included), results below the
+// normal range or overflowing, a significand of all ones rounded up to the
+// next power of two; add_general then computes the result.
+//
+// Same exact-then-round computation as add_general, one bit lower: the
+// operands sit in 128 bits with one bit of headroom (A = ma * 2^63,
+// B = mb * 2^(63-d), exact for d < 64), so a carry lands in bit 127 instead
+// of leaving the word, and addition and subtraction share one normalising
+// left shift by clz (0 or 1 after an addition).  For d >= 66 B is dropped:
+// it lies below a quarter of A's ulp and RNE returns A.
+// v_bitop3_b32 (gfx950): bit i of IMM is the result for the input bits
+// (a, b, c) = (i >> 2, i >> 1, i) & 1.  The host build (tests) evaluates the
+// same truth table.
+template <unsigned IMM>
+OSGPU_HD inline uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 8; i++)
+        if ((IMM >> i) & 1) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+#endif
+}
+
+// (x & z) ^ m per 32-bit word: bit (a=x, b=z, c=m) -> (a & b) ^ c
+constexpr unsigned kAndXor = 0x78;
+
+OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
+{
+    const bool swap = b.e > a.e || (b.e == a.e && b.m > a.m);  // |A| >= |B|
+    const uint64_t ma = swap ? b.m : a.m;
+    const uint64_t mb = swap ? a.m : b.m;
+    const uint32_t EA = swap ? b.e : a.e;
+    const uint32_t d = EA - (swap ? a.e : b.e);
+    const uint32_t sign = swap ? b.s : a.s;
+    const unsigned sh = d & 63;
+    const uint64_t ah = ma >> 1, bh = (mb >> sh) >> 1, bl = mb << (63 - sh);
+    // B is dropped for d >= 64 (mask z) and complemented for a subtraction
+    // (mask m): one three-input bit operation per word, (b & z) ^ m; the + 1
+    // of the two's complement rides in as the carry into the lowest word
+    // (whose A word is zero)
+    const bool sub = a.s != b.s;
+    const uint32_t m = sub ? ~0u : 0u;
+    const uint32_t z = (uint32_t) ((int32_t) (d - 64) >> 31);  // d < 64: all ones
+    unsigned c0, c1, c2, c3;
+    const uint32_t s0 = __builtin_addc(0u, bitop3<kAndXor>((uint32_t) bl, z, m), sub ? 1u : 0u, &c1);
+    const uint32_t s1 = __builtin_addc((uint32_t) ma << 31, bitop3<kAndXor>((uint32_t) (bl >> 32), z, m), c1, &c2);
+    const uint32_t s2 = __builtin_addc((uint32_t) ah, bitop3<kAndXor>((uint32_t) bh, z, m), c2, &c3);
+    const uint32_t s3 = __builtin_addc((uint32_t) (ah >> 32), bitop3<kAndXor>((uint32_t) (bh >> 32), z, m), c3, &c0);
+    (void) c0;  // no carry out of bit 127 for an addition (headroom); a subtraction's is dropped
+    uint64_t hi = ((uint64_t) s3 << 32) | s2, lo = ((uint64_t) s1 << 32) | s0;
+    const bool cancel = hi == 0;
+    const int lz = __builtin_clzg(hi, 64);  // 64 only when cancel (flagged)
+    const unsigned l6 = lz & 63;
+    hi = (hi << l6) | ((lo >> 1) >> (63 - l6));
+    lo <<= l6;
+    const uint32_t Em1 = EA - (uint32_t) lz;  // E - 1, E = EA + 1 - lz
+    // round to nearest even at bit 64: up when lo > 2^63, or lo == 2^63 and
+    // hi is odd; the carry out of hi (all ones rounded up) is the wrap case
+    const bool up = lo > (1ull << 63) - (hi & 1);
+    unsigned w1, wrap;
+    const uint32_t h0 = __builtin_addc((uint32_t) hi, 0u, up ? 1u : 0u, &w1);
+    const uint32_t h1 = __builtin_addc((uint32_t) (hi >> 32), 0u, w1, &wrap);
+    *r = XU{((uint64_t) h1 << 32) | h0, Em1 + 1, sign};
+    // 1 <= E <= 0x7ffe in one unsigned test (underflow, overflow)
+    return d - 64u >= 2u && !cancel && Em1 < kEmax - 1 && !wrap;
+}
+
+// The fast form when it applies, else the general add (out of line: a fold
+// of P inputs makes P(P-1) adds, and the rarely taken general path inlined
+// into each of them made a long double team kernel of 24 K instructions,
+// beyond the instruction cache).
+OSGPU_HD inline XU add_u(XU a, XU b)
+{
+    XU r;
+    if (normal_u(a) && normal_u(b) && add_fast(a, b, &r)) return r;
+    return unpack_u(add_general(pack_u(a), pack_u(b)));
+}
+
+OSGPU_HD inline X80 add(X80 a, X80 b) { return pack_u(add_u(unpack_u(a), unpack_u(b))); }
+
+OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD) return defnan();
+    if (is_nan(ca) || is_nan(cb)) return nan_pick(a, ca, b, cb);
+    const uint32_t sa = (a.se >> 15) & 1, sb = (b.se >> 15) & 1;
+    if (ca == C_INF || cb == C_INF) {
+        if (ca == C_INF && cb == C_INF) return sa == sb ? a : defnan();
+        return ca == C_INF ? a : b;
+    }
+    if (ca == C_ZERO && cb == C_ZERO) return X80{0, (sa & sb) << 15};
+    int Ea = (int) (a.se & kEmax), Eb = (int) (b.se & kEmax);
+    Ea = Ea ? Ea : 1;
+    Eb = Eb ? Eb : 1;
+    uint64_t ma = a.m, mb = b.m;
+    uint32_t sign = sa;
+    if (cb == C_ZERO) { mb = 0; Eb = Ea; }
+    if (ca == C_ZERO) { ma = 0; Ea = Eb; }
+    // order by magnitude: |a| >= |b|
+    if (Eb > Ea || (Eb == Ea && mb > ma)) {
+        uint64_t tm = ma; ma = mb; mb = tm;
+        int te = Ea; Ea = Eb; Eb = te;
+        sign = sb;
+    }
+    const int d = Ea - Eb;
+    const u128 A = (u128) ma << 64;
+    u128 B = (u128) mb << 64;
+    if (d >= 128) {
+        B = (mb != 0) ? 1 : 0;
+    } else if (d > 0) {
+        const bool sticky = (B << (128 - d)) != 0;
+        B = (B >> d) | (u128) (sticky ? 1 : 0);
+    }
+    int E = Ea;
+    u128 S;
+    if (sa == sb) {
+        S = A + B;
+        if (S < A) {                             // carry out of bit 127
+            S = (S >> 1) | (S & 1) | ((u128) 1 << 127);
+            E += 1;
+        }
+    } else {
+        S = A - B;
+        if (S == 0) return X80{0, 0};            // exact cancellation: +0 (RNE)
+    }
+    const int lz = clz128(S);
+    S <<= lz;
+    E -= lz;
+    // value = S * 2^(E - bias - 127): the exponent convention above treats
+    // the 128-bit S as significand bits 127..0 with J at 127
+    return round_pack(sign, E, S);
+}
+
+OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b);
+
+// mul of two NORMAL operands (the caller checks), straight-line: the exact
+// 128-bit product of two significands with J set lies in [2^126, 2^128), so
+// the renormalising shift is 0 or 1 (a select), then one RNE rounding at bit
+// 64 -- the general path's computation without its classification and
+// variable shifts.  false: the product leaves the normal range (denormal or
+// infinity) or its rounding carries out of the significand; mul_general
+// computes it.
+OSGPU_HD inline bool mul_fast(XU a, XU b, XU *r)
+{
+    const u128 P = (u128) a.m * (u128) b.m;
+    uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
+    const bool top = (hi >> 63) != 0;
+    const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
+    hi = top ? hi : h1;
+    lo = top ? lo : l1;
+    // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = S * 2^(E-bias-127)
+    int E = (int) a.e + (int) b.e - kBias + (top ? 1 : 0);
+    const bool low = E < 1;
+    hi += lo > (1ull << 63) - (hi & 1) ? 1 : 0;  // RNE at bit 64 (add_fast)
+    const bool wrap = hi == 0;
+    *r = XU{hi, (uint32_t) E, a.s ^ b.s};
+    return !low && !wrap && E < (int) kEmax;
+}
+
+OSGPU_HD inline XU mul_u(XU a, XU b)
+{
+    XU r;
+    if (normal_u(a) && normal_u(b) && mul_fast(a, b, &r)) return r;
+    return unpack_u(mul_general(pack_u(a), pack_u(b)));
+}
+
+OSGPU_HD inline X80 mul(X80 a, X80 b) { return pack_u(mul_u(unpack_u(a), unpack_u(b))); }
+
+OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD) return defnan();
+    if (is_nan(ca) || is_nan(cb)) return nan_pick(a, ca, b, cb);
+    const uint32_t s = ((a.se ^ b.se) >> 15) & 1;
+    if (ca == C_INF || cb == C_INF) {
+        if (ca == C_ZERO || cb == C_ZERO) return defnan();
+        return X80{1ull << 63, (s << 15) | kEmax};
+    }
+    if (ca == C_ZERO || cb == C_ZERO) return X80{0, s << 15};
+    int Ea = (int) (a.se & kEmax), Eb = (int) (b.se & kEmax);
+    Ea = Ea ? Ea : 1;
+    Eb = Eb ? Eb : 1;
+    u128 P = (u128) a.m * (u128) b.m;            // exact, nonzero
+    const int lz = clz128(P);
+    P <<= lz;
+    // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = P * 2^(Ea+Eb-2bias-126-lz)
+    //   = S * 2^(E - bias - 127)  =>  E = Ea + Eb - bias + 1 - lz
+    const int E = Ea + Eb - kBias + 1 - lz;
+    return round_pack(s, E, P);
+}
+
+// Every member's fold of a P-PE sum (OP 0) or prod (OP 1) of one element,
+// each in its own order (src/reductions.c:79-111: PE q starts from its own
+// x_q, then x_0, x_1, ... skipping q).  x87 add and mul are commutative bit
+// for bit (same rounding of the same exact value; nan_pick is symmetric), so
+// member 1's fold x1 op x0 op x2 ... equals member 0's: P-1 folds, not P.
+//
+// The folds advance in rounds: round t applies every fold's t-th operand
+// with the straight-line fast op, so the P-1 independent chains interleave
+// in one instruction stream (ILP for a VALU-bound kernel); only when some
+// lane of the wave has an operand or result outside the fast op's range
+// does the round take the general op, for those folds and lanes.  A fold
+// whose running value leaves the normal range stays on the general op
+// (`slow`) until it is normal again.
+template <int OP, int P>
+OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
+{
+    constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
+    XU u[P];
+    bool nrm[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        u[p] = unpack_u(x[p]);
+        nrm[p] = normal_u(u[p]);
+    }
+    XU acc[NF];
+    bool slow[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        const int q = f == 0 ? 0 : f + 1;
+        acc[f] = u[q];
+        slow[f] = !nrm[q];
+    }
+#pragma unroll
+    for (int t = 0; t < P - 1; t++) {
+        XU res[NF];
+        bool ok[NF];
+        bool all = true;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            const int q = f == 0 ? 0 : f + 1;
+            const int j = t < q ? t : t + 1;  // q's t-th operand
+            const bool fast = OP == 0 ? add_fast(acc[f], u[j], &res[f])
+                                      : mul_fast(acc[f], u[j], &res[f]);
+            ok[f] = fast && !slow[f] && nrm[j];
+            all = all && ok[f];
+        }
+        if (!all) {
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                if (!ok[f]) {
+                    const int q = f == 0 ? 0 : f + 1;
+                    const int j = t < q ? t : t + 1;
+                    res[f] = unpack_u(OP == 0 ? add_general(pack_u(acc[f]), pack_u(u[j]))
+                                              : mul_general(pack_u(acc[f]), pack_u(u[j])));
+                    slow[f] = !normal_u(res[f]);
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; f++) acc[f] = res[f];
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++) out[f == 0 ? 0 : f + 1] = pack_u(acc[f]);
+    out[1] = out[0];
+}
+
+OSGPU_HD inline bool less(X80 a, X80 b);
+
+// Every member's fold of a P-PE max (OP 5) or min (OP 6) of one element.
+// The fold acc = (acc < b ? acc : b) (min; > for max, miscops.c:80-105)
+// visits x_q, then x_0, x_1, ... skipping q, and keeps the LAST visited
+// element with the extreme value (a tie hands over to the incoming b).  So
+// with t1 = the highest index holding the extreme and t2 the next highest,
+// member q gets x_t1 unless q == t1, which gets x_t2 (x_t1 if alone) -- the
+// same encodings the P(P-1) compares select, from P compares.  Values are
+// ordered by a 16+64-bit key (positive: 0x8000|e : m; negative:
+// 0x7fff-e : ~m; zeros as +0), which is fcomi's order on zeros, denormals,
+// normals and infinities.  Any NaN or unsupported / pseudo-denormal encoding
+// in the element sends it to the compare-by-compare folds.
+template <int OP, int P>
+OSGPU_HD inline void team_fold_minmax(const X80 (&x)[P], X80 (&out)[P])
+{
+    uint32_t kh[P];
+    uint64_t kl[P];
+    bool ord = true;
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        const uint32_t e = x[p].se & kEmax;
+        const uint64_t m = x[p].m;
+        const bool J = (m >> 63) != 0;
+        ord = ord && (e == 0 ? !J : (e == kEmax ? m == (1ull << 63) : J));
+        const bool neg = ((x[p].se >> 15) & 1) && (e | m) != 0;
+        kh[p] = neg ? kEmax - e : 0x8000u | e;
+        kl[p] = neg ? ~m : m;
+    }
+    if (!ord) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+            X80 acc = x[q];
+#pragma unroll
+            for (int j = 0; j < P; j++)
+                if (j != q) {  // field by field: a select of whole structs
+                               // makes the compiler address x through scratch
+                    const bool keep = OP == 5 ? less(x[j], acc) : less(acc, x[j]);
+                    acc.m = keep ? acc.m : x[j].m;
+                    acc.se = keep ? acc.se : x[j].se;
+                }
+            out[q] = acc;
+        }
+        return;
+    }
+    uint32_t bh = kh[0];
+    uint64_t bl = kl[0];
+#pragma unroll
+    for (int p = 1; p < P; p++) {
+        const bool lt = kh[p] < bh || (kh[p] == bh && kl[p] < bl);
+        const bool gt = kh[p] > bh || (kh[p] == bh && kl[p] > bl);
+        const bool take = OP == 5 ? gt : lt;
+        bh = take ? kh[p] : bh;
+        bl = take ? kl[p] : bl;
+    }
+    // the highest index holding it (t1, value v1) and the value at the next
+    // highest (v2; v1 when t1 is alone), carried along the scan
+    int t1 = -1;
+    bool two = false;
+    X80 v1 = x[0], v2 = x[0];
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        const bool eq = kh[p] == bh && kl[p] == bl;
+        v2.m = eq && t1 >= 0 ? v1.m : v2.m;
+        v2.se = eq && t1 >= 0 ? v1.se : v2.se;
+        two = two || (eq && t1 >= 0);
+        v1.m = eq ? x[p].m : v1.m;
+        v1.se = eq ? x[p].se : v1.se;
+        t1 = eq ? p : t1;
+    }
+    v2.m = two ? v2.m : v1.m;
+    v2.se = two ? v2.se : v1.se;
+#pragma unroll
+    for (int q = 0; q < P; q++) {  // member q: v1 unless q == t1
+        out[q].m = q == t1 ? v2.m : v1.m;
+        out[q].se = q == t1 ? v2.se : v1.se;
+    }
+}
+
+// fcomi ordering; false when unordered (NaN or unsupported encoding)
+OSGPU_HD inline bool less(X80 a, X80 b)
+{
+    const Cls ca = classify(a), cb = classify(b);
+    if (ca == C_BAD || cb == C_BAD || is_nan(ca) || is_nan(cb)) return false;
+    const bool za = ca == C_ZERO, zb = cb == C_ZERO;
+    if (za && zb) return false;
+    const bool na = !za && ((a.se >> 15) & 1), nb = !zb && ((b.se >> 15) & 1);
+    if (na != nb) return na;
+    // magnitude keys (E, m): zero < denormal/pseudo-denormal (E=1) < ...
+    uint32_t ea = za ? 0 : ((a.se & kEmax) ? (a.se & kEmax) : 1);
+    uint32_t eb = zb ? 0 : ((b.se & kEmax) ? (b.se & kEmax) : 1);
+    const uint64_t ma = za ? 0 : a.m, mb = zb ? 0 : b.m;
+    const bool mag_lt = ea < eb || (ea == eb && ma < mb);
+    const bool mag_gt = ea > eb || (ea == eb && ma > mb);
+    return na ? mag_gt : mag_lt;
+}
+
+}  // namespace x87
+}  // namespace osgpu

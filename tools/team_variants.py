@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""team_variants.py -- A/B of team-kernel builds over every type at 2, 4
+and 8 members.  Not part of the product.
+
+  python tools/team_variants.py build      (here, on the CPU)
+      compiles team.hip (and combine.hip) with each variant's -D flags into
+      tools/variants/<name>/libosgpu_reduce.so, linked with the tree's other
+      objects; "git:<rev>" variants take team.hip/combine.hip/elem_ops.hpp
+      from that revision (the baseline before a change)
+  python tools/team_variants.py run        (on the GPU box)
+      every build loaded into one process, interleaved on the same arrays:
+      team_vec_kernel through osgpu_team_combine, one launch over n elements
+      per member, HIP-event spans over REPS launches, TV_ROUNDS rounds; one
+      JSON line per (variant, type, P) with the median and the fraction of
+      8 TB/s for 2*P*n*s bytes.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc")
+VAR = os.path.join(ROOT, "tools", "variants")
+FL = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+      "-fno-fast-math"]
+VARIANTS = {
+    "base": ("git:HEAD", []),
+    "bf": (None, []),
+    "bf_u2_2_u8_4": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=4"]),
+    "bf_u2_2_u8_4g2": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=2"]),
+}
+OTHERS = ["fused.o", "verify.o", "longdouble.o", "copy.o", "runtime.o", "heap.o",
+          "shmem_reduce.o", "shmem_collect.o"]
+
+
+def build():
+    subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
+    procs = []
+    for name, (rev, flags) in VARIANTS.items():
+        d = os.path.join(VAR, name)
+        os.makedirs(d, exist_ok=True)
+        src = CSRC
+        if rev:
+            src = os.path.join(d, "src")
+            os.makedirs(src, exist_ok=True)
+            for f in ("team.hip", "combine.hip", "elem_ops.hpp", "combine.hpp"):
+                txt = subprocess.run(["git", "show", f"{rev[4:]}:test-resilient-osss-ucx_amd/csrc/{f}"],
+                                     cwd=ROOT, check=True, capture_output=True).stdout
+                open(os.path.join(src, f), "wb").write(txt)
+        for f in ("team", "combine"):
+            procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + FL + flags +
+                                          ["-c", os.path.join(src, f + ".hip"), "-o",
+                                           os.path.join(d, f + ".o")]))
+    assert all(p.wait() == 0 for p in procs)
+    for name in VARIANTS:
+        d = os.path.join(VAR, name)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                        os.path.join(d, "libosgpu_reduce.so"), os.path.join(d, "team.o"),
+                        os.path.join(d, "combine.o")] + [os.path.join(CSRC, o) for o in OTHERS] +
+                       ["-lrccl", "-ldl", "-lpthread"], check=True)
+        print("built", name)
+
+
+def run():
+    """Every variant loaded into ONE process (each build its own module,
+    RTLD_LOCAL), the variants interleaved launch block by launch block on the
+    same arrays: box and allocation effects hit them alike.  Per (type, P):
+    TV_ROUNDS rounds of (for each variant: a HIP-event span over REPS
+    launches); the median per variant."""
+    import ctypes
+    import torch
+    torch.cuda.init()
+    names = os.environ.get("TV_NAMES", ",".join(VARIANTS)).split(",")
+    libs = {}
+    for name in names:
+        L = ctypes.CDLL(os.path.join(VAR, name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
+        L.osgpu_team_combine.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        libs[name] = L
+    reps = int(os.environ.get("REPS", "10"))
+    rounds = int(os.environ.get("TV_ROUNDS", "5"))
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    types = (("double", 5, torch.float64), ("float", 4, torch.float32),
+             ("int", 1, torch.int32), ("short", 0, torch.int16), ("long", 2, torch.int64),
+             ("complexf", 7, torch.complex64), ("complexd", 8, torch.complex128))
+    only = os.environ.get("TV_TYPES")
+    nbytes = int(os.environ.get("TV_BYTES", str(512 << 20)))
+    for P in (2, 4, 8):
+        for t, code, dt in types:
+            if only and t not in only.split(","):
+                continue
+            es = torch.empty(0, dtype=dt).element_size()
+            n = nbytes // es
+            g = torch.Generator(device="cuda").manual_seed(5)
+            xs = []
+            for _ in range(P):
+                x = torch.empty(n, dtype=dt, device="cuda")
+                if dt.is_floating_point or dt.is_complex:
+                    x.view(torch.float32 if dt in (torch.float32, torch.complex64)
+                           else torch.float64).uniform_(1, 2, generator=g)
+                else:
+                    x.random_(-100, 100, generator=g)
+                xs.append(x)
+            ys = [torch.empty(n, dtype=dt, device="cuda") for _ in range(P)]
+            S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in xs])
+            D = (ctypes.c_void_p * P)(*[y.data_ptr() for y in ys])
+            acc = xs[0].clone()
+            for x in xs[1:]:
+                acc = acc + x
+            torch.cuda.synchronize()
+            times = {name: [] for name in names}
+            exact = {}
+            for name, L in libs.items():
+                for _ in range(2):
+                    assert L.osgpu_team_combine(code, 0, P, D, S, n, sp) == 0
+                torch.cuda.synchronize()
+                # member 0's result: x0 + x1 + ... in order (complexf: the
+                # compiled order adds imaginary parts as b.im + a.im -- same
+                # values for these finite inputs)
+                exact[name] = bool(torch.equal(ys[0], acc))
+            for _ in range(rounds):
+                for name, L in libs.items():
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(reps):
+                        L.osgpu_team_combine(code, 0, P, D, S, n, sp)
+                    e1.record(st)
+                    e1.synchronize()
+                    times[name].append(e0.elapsed_time(e1) * 1e3 / reps)
+            for name in names:
+                us = sorted(times[name])[len(times[name]) // 2]
+                print(json.dumps({"variant": name, "type": t, "P": P, "n": n, "us": us,
+                                  "frac": 2 * P * n * es / us / 8e6,
+                                  "spread_us": [min(times[name]), max(times[name])],
+                                  "member0_exact": exact[name]}), flush=True)
+            del xs, ys, acc
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]]()
