@@ -309,10 +309,11 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     every source once, writes every target (PE q: x_q + the others in
     ascending order).  Algorithmic bytes 2*P*n*8 per launch.  HIP events on
     the launch stream.  Beside it the same-mix ceiling: the copy kernel
-    (csrc/copy.hip) moving P ranges of n*8 bytes in one launch -- P read
-    and P write streams over the same bytes, nothing folded."""
+    (csrc/copy.hip) moving P ranges of n*8 bytes in one launch, its tiles
+    dealt round-robin over the ranges -- P read and P write streams at once
+    over the same bytes, nothing folded."""
     dev = torch.device("cuda:0")
-    g = torch.Generator(device=dev).manual_seed(11)
+    g = torch.Generator(device=dev).manual_seed(11 + P)
     srcs_t = [torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0, generator=g)
               for _ in range(P)]
     dsts_t = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(P)]
@@ -358,7 +359,7 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     cavg = span_per_launch(torch, st, copy, reps)
     B = 2 * P * n * 8
     kern = f"team_vec_kernel<double, 0, {P}, true>"
-    tr = load_traffic(kern, n if P == 2 else None)
+    tr = load_traffic(kern, n)
     frac = B / kavg / 1e9 / HBM_PEAK_GBS
     cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -369,14 +370,34 @@ def team_kernel_rate(L, torch, n, reps, P=2):
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
            "kernel_min_us_per_launch_events": min(ks) * 1e6,
            "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact_sample": exact,
-           "copy_ceiling_same_mix": {"kernel": "copy_vec_kernel", "ranges": P,
-                                     "bytes_per_range": n * 8, "us": cavg * 1e6,
+           "copy_ceiling_same_mix": {"kernel": "copy_vec_kernel (ranges dealt round-robin)",
+                                     "ranges": P, "bytes_per_range": n * 8, "us": cavg * 1e6,
                                      "frac_of_8TBs": cfrac},
            "frac_of_copy_ceiling": frac / cfrac,
            "note": f"one launch over all nreduce elements = the {P} PEs' shard launches of a "
                    f"{P}-PE call; {P} reads + {P} writes of 8 B per element"}
     del srcs_t, dsts_t
     torch.cuda.empty_cache()
+    return out
+
+
+def team_placements(L, torch, n, reps, P, trials=3):
+    """team_kernel_rate on `trials` fresh allocations (the arrays freed and
+    allocated again: new physical pages).  The rate of 2P streams read and
+    written in lockstep depends on where the pages land -- the same kernel
+    and the round-robin copy both move 0.72-0.84 of 8 TB/s at P = 2..8
+    across placements (tools/tune_team.hip `layouts`,
+    profiles/r03_team_layouts.jsonl) -- so the line reports every trial and
+    the medians."""
+    runs = [team_kernel_rate(L, torch, n, reps, P) for _ in range(trials)]
+    med = sorted(runs, key=lambda r: r["frac_of_copy_ceiling"])[len(runs) // 2]
+    out = dict(med)
+    out["placements"] = [{"frac": r["frac"], "copy_frac": r["copy_ceiling_same_mix"]["frac_of_8TBs"],
+                          "frac_of_copy_ceiling": r["frac_of_copy_ceiling"],
+                          "kernel_avg_us": r["kernel_avg_us"]} for r in runs]
+    out["placements_note"] = (f"{trials} allocations; the fields above are the trial with the "
+                              f"median frac_of_copy_ceiling")
+    out["bit_exact_sample"] = all(r["bit_exact_sample"] for r in runs)
     return out
 
 
@@ -609,9 +630,9 @@ def bench_single(args):
     except Exception as e:  # report, never hide
         res["roofline_team"] = {"error": repr(e)}
     res["roofline_team_by_members"] = {}
-    for P in ((4, 8) if not args.no_extra else ()):
+    for P in ((2, 4, 8) if not args.no_extra else ()):
         try:
-            res["roofline_team_by_members"][str(P)] = team_kernel_rate(
+            res["roofline_team_by_members"][str(P)] = team_placements(
                 L, torch, n, min(args.steps, 20), P)
         except Exception as e:  # report, never hide
             res["roofline_team_by_members"][str(P)] = {"error": repr(e)}

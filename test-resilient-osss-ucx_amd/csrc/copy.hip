@@ -12,7 +12,13 @@
 // Layout of a launch: each segment gets ceil(body / (256 * U)) workgroups of
 // 256 lanes, each lane U 16-byte vectors (all loads issued before the first
 // store, non-temporal both ways -- the shape tools/tune_combine.hip found
-// fastest for the combine).  Vectors are aligned on the DESTINATION; the
+// fastest for the combine).  The segments' tiles are dealt round-robin
+// (workgroup b -> segment b % m, for as many rounds as the smallest segment
+// has tiles; the rest of the larger segments follow, segment by segment):
+// dispatch runs workgroups roughly in order, so with segments one after
+// another the ~2 K workgroups resident at any moment would all stream ONE
+// segment -- over xGMI one peer link at a time while the others idle.
+// Round-robin keeps every segment (every peer's link) streaming at once.  Vectors are aligned on the DESTINATION; the
 // source may sit at any 4-byte phase (gfx950 serves dword-aligned
 // global_load_dwordx4), so a 32-bit collect whose block offsets are not
 // 16-byte multiples stays on the vector path.  The first workgroup of a
@@ -39,7 +45,8 @@ struct SegTable {
     const char *src[kMaxCopySegs];
     char *dst[kMaxCopySegs];
     size_t bytes[kMaxCopySegs];
-    unsigned first_block[kMaxCopySegs + 1];
+    unsigned first_block[kMaxCopySegs + 1];  // of the blocked part (tiles past `rounds`)
+    unsigned rounds;                          // round-robin rounds (vector kernel)
     int n;
 };
 
@@ -54,7 +61,19 @@ __device__ __forceinline__ int find_seg(const SegTable &t, unsigned b)
 
 __global__ __launch_bounds__(kThreads) void copy_vec_kernel(SegTable t)
 {
-    const int k = find_seg(t, blockIdx.x);
+    // round-robin part first: block b -> segment b % n, tile b / n; then
+    // every segment's tiles from `rounds` on, segment after segment
+    const unsigned inter = t.rounds * (unsigned) t.n;
+    int k;
+    unsigned lb;
+    if (blockIdx.x < inter) {
+        k = (int) (blockIdx.x % (unsigned) t.n);
+        lb = blockIdx.x / (unsigned) t.n;
+    } else {
+        const unsigned b = blockIdx.x - inter;
+        k = find_seg(t, b);
+        lb = t.rounds + (b - t.first_block[k]);
+    }
     const char *s = t.src[k];
     char *d = t.dst[k];
     const size_t bytes = t.bytes[k];
@@ -62,7 +81,6 @@ __global__ __launch_bounds__(kThreads) void copy_vec_kernel(SegTable t)
     if (head > bytes) head = bytes;
     const size_t nvec = (bytes - head) / 16;
     const size_t tail0 = head + nvec * 16;
-    const unsigned lb = blockIdx.x - t.first_block[k];
     if (lb == 0) {
         const unsigned x = threadIdx.x;
         if (x < head) d[x] = s[x];
@@ -117,7 +135,22 @@ hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t stream)
         nb += (unsigned) blocks;
     }
     if (vt.n) {
-        vt.first_block[vt.n] = vblocks;
+        // round-robin rounds = the smallest segment's tile count; the
+        // blocked table then holds only each segment's tiles beyond them
+        unsigned rounds = ~0u;
+        for (int i = 0; i < vt.n; i++) {
+            const unsigned next = i + 1 < vt.n ? vt.first_block[i + 1] : vblocks;
+            rounds = next - vt.first_block[i] < rounds ? next - vt.first_block[i] : rounds;
+        }
+        unsigned nb = 0;
+        for (int i = 0; i < vt.n; i++) {
+            const unsigned next = i + 1 < vt.n ? vt.first_block[i + 1] : vblocks;
+            const unsigned tiles = next - vt.first_block[i];
+            vt.first_block[i] = nb;
+            nb += tiles - rounds;
+        }
+        vt.first_block[vt.n] = nb;
+        vt.rounds = rounds;
         hipLaunchKernelGGL(copy_vec_kernel, dim3(vblocks), dim3(kThreads), 0, stream, vt);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -255,3 +255,36 @@ def test_random_collectives(block):
         mode, kind, bits, setdef, nelems, root, seed = _random_case(k)
         with host_path(mode):
             _run_case(mode != "device", kind, bits, setdef, nelems, root=root, seed=seed)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_copy_kernel_segment_layouts(seed):
+    """osgpu_copy directly: up to 9 segments (a second launch past 8) of
+    mixed sizes -- empty, below one vector, unaligned heads and tails,
+    one tile, many tiles, very unequal -- at every 4-byte source phase and
+    byte phases (the byte kernel).  The segments' tiles are dealt
+    round-robin for as many rounds as the smallest segment has, then
+    segment by segment (copy.hip); every destination byte must equal its
+    source and nothing outside the ranges may change."""
+    import torch
+    rng = np.random.default_rng(seed)
+    nseg = int(rng.integers(1, 10))
+    tile = 256 * 4 * 16
+    sizes = [int(rng.choice([0, 3, 15, 16, 17, 1000, tile - 1, tile, tile + 5, 3 * tile + 7,
+                             int(rng.integers(1, 40 * tile))])) for _ in range(nseg)]
+    pad = 64
+    total = sum(s + 2 * pad for s in sizes) + 64
+    src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda")
+    dst = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    srcs, dsts, off, want = [], [], 16, dst.clone()
+    for i, s in enumerate(sizes):
+        so = off + int(rng.choice([0, 4, 8, 12] if i % 3 else [1, 2, 3]))   # byte phases too
+        do = off + int(rng.choice([0, 4, 8, 12]))
+        srcs.append(src.data_ptr() + so)
+        dsts.append(dst.data_ptr() + do)
+        want[do:do + s] = src[so:so + s]
+        off += s + 2 * pad
+    torch.cuda.synchronize()
+    osgpu.copy(dsts, srcs, sizes)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, want), (sizes, int((dst != want).sum()))

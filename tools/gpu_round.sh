@@ -42,11 +42,20 @@ for s in ${STEPS:-smoke tests bench prof}; do
     multi_self) step multi_self 420 python bench.py --gpus 2 --steps 5 --warmup 2 --deadline 360 ;;
     multi_self4) step multi_self4 420 python bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((16<<20)) --c4-nreduce $((64<<20)) --c5-nreduce $((16<<20)) --deadline 360 ;;
     multi8) step multi8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
+    teamlayout) step teamlayout 300 python -u tools/team_layout_probe.py && TL_P=2 step teamlayout2 300 python -u tools/team_layout_probe.py && TL_P=8 TL_N=$((32<<20)) step teamlayout8 300 python -u tools/team_layout_probe.py ;;
     teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
+    teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
     multi8_self) step multi8_self 900 python bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     multi4_s) step multi4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 200 ;;
+    prof3) step prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
+    pmc3)  step pmc3f 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3f -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+           step pmc3w 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc3w -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic.json &&
+           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team.json "team_vec_kernel<double, 0, 2, true>" 32 &&
+           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team4.json "team_vec_kernel<double, 0, 4, true>" 64 &&
+           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team8.json "team_vec_kernel<double, 0, 8, true>" 128 ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $((64<<20)) gpurun_out/traffic.json &&

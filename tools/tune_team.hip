@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -132,6 +133,24 @@ __global__ __launch_bounds__(256) void copy_kernel(Ptrs<P> a, size_t nvec, unsig
         if (base + u * 256 < nvec) __builtin_nontemporal_store(v[u], d + base + u * 256);
 }
 
+// the same ranges with every range streaming at once: block b copies a tile
+// of range b % P (the team kernel's 2P concurrent streams, no fold)
+template <int P>
+__global__ __launch_bounds__(256) void copy_interleaved_kernel(Ptrs<P> a, size_t nvec)
+{
+    const int r = blockIdx.x % P;
+    const size_t base = (size_t) (blockIdx.x / P) * 256 * 4 + threadIdx.x;
+    u32x4 v[4];
+    const u32x4 *s = reinterpret_cast<const u32x4 *>(a.src[r]);
+    u32x4 *d = reinterpret_cast<u32x4 *>(a.dst[r]);
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (base + u * 256 < nvec) v[u] = __builtin_nontemporal_load(s + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (base + u * 256 < nvec) __builtin_nontemporal_store(v[u], d + base + u * 256);
+}
+
 // uniform [1, 2) doubles from a hash of (array, index): data like the bench's
 __global__ void fill_kernel(double *p, size_t n, unsigned seed)
 {
@@ -186,6 +205,17 @@ static double copy_us()
     Ptrs<P> a = ptrs<P>();
     return median_us([&] {
         hipLaunchKernelGGL(copy_kernel<P>, dim3(per * P), dim3(256), 0, 0, a, nvec, per);
+    });
+}
+
+template <int P>
+static double copy_il_us()
+{
+    const size_t nvec = g_n / 2;
+    const unsigned per = (unsigned) ((nvec + 1023) / 1024);
+    Ptrs<P> a = ptrs<P>();
+    return median_us([&] {
+        hipLaunchKernelGGL(copy_interleaved_kernel<P>, dim3(per * P), dim3(256), 0, 0, a, nvec);
     });
 }
 
@@ -251,6 +281,24 @@ static void sweep()
     printf("{\"P\": %d, \"copy_us_end\": %.2f}\n", P, c2);
 }
 
+template <int P, int U, int G>
+static void layout_trial(int k)
+{
+    const size_t nvec = g_n / 2;
+    const size_t blocks = (nvec + (size_t) 256 * U - 1) / ((size_t) 256 * U);
+    Ptrs<P> a = ptrs<P>();
+    const double cb = copy_us<P>(), ci = copy_il_us<P>();
+    const double us = median_us([&] {
+        hipLaunchKernelGGL((team_kernel<P, U, G, 0, 0, 256>), dim3((unsigned) blocks), dim3(256), 0,
+                           0, a, nvec);
+    });
+    const double B = 2.0 * P * g_n * 8;
+    printf("{\"trial\": %d, \"P\": %d, \"team_frac\": %.4f, \"copy_blocked_frac\": %.4f, "
+           "\"copy_interleaved_frac\": %.4f, \"team_of_interleaved\": %.4f, \"src0\": \"%p\"}\n",
+           k, P, B / us / 8e6, B / cb / 8e6, B / ci / 8e6, ci / us, (void *) g_buf[0]);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv)
 {
     g_n = argc > 1 ? strtoull(argv[1], nullptr, 0) : (size_t) 64 << 20;
@@ -261,6 +309,23 @@ int main(int argc, char **argv)
     }
     CK(hipDeviceSynchronize());
     const int passes = argc > 3 ? atoi(argv[3]) : 2;
+    if (argc > 4 && !strcmp(argv[4], "layouts")) {
+        // placement trials: every array freed and allocated again, then the
+        // shipped team shape, the blocked copy and the interleaved copy
+        for (int k = 0; k < passes; k++) {
+            for (int i = 0; i < 16; i++) CK(hipFree(g_buf[i]));
+            for (int i = 0; i < 16; i++) {
+                CK(hipMalloc(&g_buf[i], g_n * 8));
+                hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, g_buf[i], g_n,
+                                   (unsigned) (i + 16 * k));
+            }
+            CK(hipDeviceSynchronize());
+            layout_trial<2, 4, 4>(k);
+            layout_trial<4, 4, 4>(k);
+            layout_trial<8, 4, 2>(k);
+        }
+        return 0;
+    }
     for (int k = 0; k < passes; k++) {
         sweep<2>();
         sweep<4>();
