@@ -41,6 +41,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     r3tests) step r3tests 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_multiproc.py -k "preflight or mixed_topology or heap_reuse" ;;
     multi_self) step multi_self 420 python bench.py --gpus 2 --steps 5 --warmup 2 --deadline 360 ;;
     multi_self4) step multi_self4 420 python bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((16<<20)) --c4-nreduce $((64<<20)) --c5-nreduce $((16<<20)) --deadline 360 ;;
+    multi_tr2) step multi_tr2 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 2 --steps 5 --warmup 2 --deadline 360 ;;
     multi8) step multi8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     teamlayout) step teamlayout 300 python -u tools/team_layout_probe.py && TL_P=2 step teamlayout2 300 python -u tools/team_layout_probe.py && TL_P=8 TL_N=$((32<<20)) step teamlayout8 300 python -u tools/team_layout_probe.py ;;
     teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
