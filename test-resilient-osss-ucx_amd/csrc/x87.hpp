@@ -163,6 +163,58 @@ OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
     return d - 64u >= 2u && !cancel && !low && !wrap && E < (int) kEmax;
 }
 
+// add_fast for two NORMAL operands of the SAME sign (the caller checks):
+// an addition needs no magnitude order (it commutes exactly, so the swap is
+// by exponent alone), no complement, and its sum of A = ma * 2^63 and
+// B = mb * 2^(63-d) lies in [2^126, 2^128): the renormalising shift is 0 or
+// 1, a select instead of a clz and three variable funnel shifts.  false:
+// gaps of 64 and 65, overflow, all ones rounded up (add_general computes
+// those).  41 VALU per add against add_fast's 56 (tools/isa/).
+OSGPU_HD inline bool add_same_fast(XU a, XU b, XU *r)
+{
+    const bool swap = b.e > a.e;
+    const uint64_t ma = swap ? b.m : a.m;
+    uint64_t mb = swap ? a.m : b.m;
+    const uint32_t EA = swap ? b.e : a.e;
+    const uint32_t d = EA - (swap ? a.e : b.e);
+    mb = d >= 64 ? 0 : mb;
+    const unsigned sh = d & 63;
+    const uint64_t ah = ma >> 1, bh = (mb >> 1) >> sh, bl = mb << (63 - sh);
+    // S = A + B in 32-bit words with explicit carries; A's lowest word is 0
+    unsigned c1, c2, c3;
+    const uint32_t s1 = __builtin_addc((uint32_t) (bl >> 32), (uint32_t) ma << 31, 0u, &c1);
+    const uint32_t s2 = __builtin_addc((uint32_t) bh, (uint32_t) ah, c1, &c2);
+    const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32), (uint32_t) (ah >> 32), c2, &c3);
+    (void) c3;  // S < 2^128: no carry out (headroom)
+    uint64_t hi = ((uint64_t) s3 << 32) | s2, lo = ((uint64_t) s1 << 32) | (uint32_t) bl;
+    const bool top = (s3 >> 31) != 0;  // S >= 2^127: no shift, else one
+    const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
+    hi = top ? hi : h1;
+    lo = top ? lo : l1;
+    const uint32_t E = EA + (top ? 1u : 0u);  // EA + 1 - lz, lz = !top
+    // round to nearest even at bit 64: up iff lo + 2^63 - 1 + (hi & 1)
+    // carries out of 64 bits (lo > 2^63 - (hi & 1)); the carry out of hi
+    // when it is all ones is the wrap case
+    unsigned u1, up, w1, wrap;
+    (void) __builtin_addc((uint32_t) lo, 0xffffffffu, (unsigned) hi & 1u, &u1);
+    (void) __builtin_addc((uint32_t) (lo >> 32), 0x7fffffffu, u1, &up);
+    const uint32_t h0 = __builtin_addc((uint32_t) hi, 0u, up, &w1);
+    const uint32_t hh = __builtin_addc((uint32_t) (hi >> 32), 0u, w1, &wrap);
+    *r = XU{((uint64_t) hh << 32) | h0, E, a.s};
+    return d - 64u >= 2u && !wrap && E < kEmax;
+}
+
+// true in every lane of the wave (device), or for this element (host, where
+// team folds run one element at a time): a wave-uniform branch condition
+OSGPU_HD inline bool wave_all(bool pred)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(!pred) == 0;
+#else
+    return pred;
+#endif
+}
+
 // The fast form when it applies, else the general add (out of line: a fold
 // of P inputs makes P(P-1) adds, and the rarely taken general path inlined
 // into each of them made a long double team kernel of 24 K instructions,
@@ -287,38 +339,17 @@ OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
     return round_pack(s, E, P);
 }
 
-// Every member's fold of a P-PE sum (OP 0) or prod (OP 1) of one element,
-// each in its own order (src/reductions.c:79-111: PE q starts from its own
-// x_q, then x_0, x_1, ... skipping q).  x87 add and mul are commutative bit
-// for bit (same rounding of the same exact value; nan_pick is symmetric), so
-// member 1's fold x1 op x0 op x2 ... equals member 0's: P-1 folds, not P.
-//
-// The folds advance in rounds: round t applies every fold's t-th operand
-// with the straight-line fast op, so the P-1 independent chains interleave
-// in one instruction stream (ILP for a VALU-bound kernel); only when some
-// lane of the wave has an operand or result outside the fast op's range
-// does the round take the general op, for those folds and lanes.  A fold
-// whose running value leaves the normal range stays on the general op
-// (`slow`) until it is normal again.
-template <int OP, int P>
-OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
+// The rounds of every member's fold (team_fold_sum_prod below).  ADD_ONLY:
+// every input of the element carries one sign, so every fold adds like
+// signs throughout (the exact sum of two values of sign s has sign s; a
+// NaN or infinity, whose sign may differ, is never normal, and a fold whose
+// value is not normal stays on the general op) -- the addition-only fast
+// add applies to every round.
+template <int OP, int P, bool ADD_ONLY>
+OSGPU_HD inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&acc)[P - 1],
+                                 bool (&slow)[P - 1])
 {
-    constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
-    XU u[P];
-    bool nrm[P];
-#pragma unroll
-    for (int p = 0; p < P; p++) {
-        u[p] = unpack_u(x[p]);
-        nrm[p] = normal_u(u[p]);
-    }
-    XU acc[NF];
-    bool slow[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) {
-        const int q = f == 0 ? 0 : f + 1;
-        acc[f] = u[q];
-        slow[f] = !nrm[q];
-    }
+    constexpr int NF = P - 1;
 #pragma unroll
     for (int t = 0; t < P - 1; t++) {
         XU res[NF];
@@ -328,8 +359,9 @@ OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
         for (int f = 0; f < NF; f++) {
             const int q = f == 0 ? 0 : f + 1;
             const int j = t < q ? t : t + 1;  // q's t-th operand
-            const bool fast = OP == 0 ? add_fast(acc[f], u[j], &res[f])
-                                      : mul_fast(acc[f], u[j], &res[f]);
+            const bool fast = OP == 1 ? mul_fast(acc[f], u[j], &res[f])
+                              : ADD_ONLY ? add_same_fast(acc[f], u[j], &res[f])
+                                         : add_fast(acc[f], u[j], &res[f]);
             ok[f] = fast && !slow[f] && nrm[j];
             all = all && ok[f];
         }
@@ -348,6 +380,49 @@ OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
 #pragma unroll
         for (int f = 0; f < NF; f++) acc[f] = res[f];
     }
+}
+
+// Every member's fold of a P-PE sum (OP 0) or prod (OP 1) of one element,
+// each in its own order (src/reductions.c:79-111: PE q starts from its own
+// x_q, then x_0, x_1, ... skipping q).  x87 add and mul are commutative bit
+// for bit (same rounding of the same exact value; nan_pick is symmetric), so
+// member 1's fold x1 op x0 op x2 ... equals member 0's: P-1 folds, not P.
+//
+// The folds advance in rounds: round t applies every fold's t-th operand
+// with the straight-line fast op, so the P-1 independent chains interleave
+// in one instruction stream (ILP for a VALU-bound kernel); only when some
+// lane of the wave has an operand or result outside the fast op's range
+// does the round take the general op, for those folds and lanes.  A fold
+// whose running value leaves the normal range stays on the general op
+// (`slow`) until it is normal again.  A sum whose inputs all carry one sign
+// in every lane of the wave (sums of same-sign data) runs every round on
+// the addition-only fast add (add_same_fast; chosen once per element, a
+// wave-uniform branch).
+template <int OP, int P>
+OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
+{
+    constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
+    XU u[P];
+    bool nrm[P];
+    bool same = OP == 0;
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        u[p] = unpack_u(x[p]);
+        nrm[p] = normal_u(u[p]);
+        same = same && u[p].s == u[0].s;
+    }
+    XU acc[NF];
+    bool slow[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        const int q = f == 0 ? 0 : f + 1;
+        acc[f] = u[q];
+        slow[f] = !nrm[q];
+    }
+    if (OP == 0 && wave_all(same))
+        fold_rounds<OP, P, true>(u, nrm, acc, slow);
+    else
+        fold_rounds<OP, P, false>(u, nrm, acc, slow);
 #pragma unroll
     for (int f = 0; f < NF; f++) out[f == 0 ? 0 : f + 1] = pack_u(acc[f]);
     out[1] = out[0];

@@ -186,6 +186,38 @@ def test_team_fold_rounds(x87, op, P):
 
 
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("sign", [0, 1])
+def test_team_fold_same_sign(x87, sign, P):
+    """Sums whose operands all share one sign take the addition-only fast
+    add (x87.hpp add_same_fast, chosen per round when every fold of every
+    lane adds like signs): exponent gaps across the 64-bit seams, carries
+    out of the significand (2^64 - small + 2^64 - small), values near
+    overflow and on the denormal grid (general path), against the
+    reference's per-PE fold order."""
+    n = 40_000
+    srcs = []
+    for p in range(P):
+        a, b = _pairs(["unit", "overflow", "underflow"][p % 3], n)
+        raw = O.value_bytes(a if p % 2 else b).reshape(-1, 10).copy()
+        x = O.value_bytes(raw_random(n, 700 + p, "near")).reshape(-1, 10)
+        k = O.splitmix64(800 + p, n)
+        pick = (k % np.uint64(3)) == np.uint64(0)
+        raw[pick] = x[pick]
+        raw[:, 9] = (raw[:, 9] & 0x7F) | (0x80 if sign else 0)   # one sign everywhere
+        srcs.append(np.ascontiguousarray(O.from_value_bytes("longdouble", raw.reshape(-1))))
+    want = O.to_all("longdouble", "sum", srcs)
+    got = [np.zeros_like(srcs[0]) for _ in range(P)]
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in srcs])
+    dp = (ctypes.c_void_p * P)(*[g.ctypes.data for g in got])
+    assert x87.x87check_team(0, P, sp, dp, n) == 0
+    for q in range(P):
+        w = O.value_bytes(want[q]).reshape(-1, 10)
+        g = O.value_bytes(got[q]).reshape(-1, 10)
+        bad = np.nonzero((w != g).any(1))[0]
+        assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
 @pytest.mark.parametrize("op", ["max", "min"])
 def test_team_fold_minmax(x87, op, P):
     """The team kernel's max / min (x87.hpp team_fold_minmax: one key scan,

@@ -21,8 +21,12 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${KEXPR:+-k "$KEXPR"} ${PYTEST_ARGS} ;;
     ldpre) OSGPU_LIB_PATH=tools/ldvariant/libosgpu_pre.so step ldpre 300 python -u tools/ld_team_rate.py ;;
+    ldtest) step ldtest 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fuzz.py ;;
     ldrate) step ldrate 300 python -u tools/ld_team_rate.py &&
             TR_TYPE=longdouble step ldcall 300 python -u tools/team_rate.py $((8<<20)) ;;
+    ldpmc3) LD_ONLY=sum/random/8 REPS=5 step ldpmc_r 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d gpurun_out/ldpmc_r -o run --output-format csv -- python3 tools/ld_team_rate.py &&
+            LD_ONLY=sum/positive/8 REPS=5 step ldpmc_p 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d gpurun_out/ldpmc_p -o run --output-format csv -- python3 tools/ld_team_rate.py &&
+            LD_ONLY=sum/ones/8 REPS=5 step ldpmc_o 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d gpurun_out/ldpmc_o -o run --output-format csv -- python3 tools/ld_team_rate.py ;;
     ldpmc) export LD_ONLY=sum/random/8 REPS=5
            step ldpmc1 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d gpurun_out/ldpmc1 -o run --output-format csv -- python3 tools/ld_team_rate.py &&
            step ldpmc2 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/ldpmc2 -o run --output-format csv -- python3 tools/ld_team_rate.py ;;

@@ -3,8 +3,9 @@
 osgpu_team_combine(longdouble, sum|prod, P) over n elements (one launch =
 every member's shard of a P-PE call), HIP events on its stream, median of
 REPS.  HBM bytes per launch 2 * P * n * 16 (P 16-B reads + P 16-B writes per
-element).  Data: "ones" (every element 1.0: exponent difference 0) or
-"random" (random 64-bit significands, exponents 2^-3..2^3, random signs).
+element).  Data: "ones" (every element 1.0: exponent difference 0), "random" (random
+64-bit significands, exponents 2^-3..2^3, random signs) or "positive" (the
+same, all positive: sums of one sign take the addition-only fast add).
 Not part of the product; JSON lines on stdout and gpurun_out/ld_team_rate.jsonl."""
 import ctypes
 import json
@@ -27,7 +28,7 @@ g = torch.Generator(device=dev).manual_seed(5)
 # LD_ONLY="sum/random/8": one case (e.g. for a PMC pass)
 only = os.environ.get("LD_ONLY")
 for op_name, op in (("sum", 0), ("prod", 1)):
-    for dist in ("ones", "random"):
+    for dist in ("ones", "random", "positive"):
         for P in (2, 4, 8):
             if only and only != f"{op_name}/{dist}/{P}":
                 continue
@@ -41,7 +42,7 @@ for op_name, op in (("sum", 0), ("prod", 1)):
                     v[:, 0] = torch.randint(-(1 << 62), 1 << 62, (n,), device=dev, generator=g) | (-(1 << 63))
                     e = 0x3fff + torch.randint(-3, 4, (n,), device=dev, generator=g)
                     sgn = torch.randint(0, 2, (n,), device=dev, generator=g) << 15
-                    v[:, 1] = e | sgn
+                    v[:, 1] = e | (sgn if dist == "random" else 0)
                 srcs.append(v)
             dsts = [torch.empty((n, 2), dtype=torch.int64, device=dev) for _ in range(P)]
             S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs])
