@@ -100,18 +100,27 @@ def load_traffic(kernel="combine_vec_kernel<double, 0, 2>", n=None):
 def cpu_baseline(n):
     """The reference's loop shape (oracle_reduce.c: copy, barrier, 64-element
     getmem chunks, per-element function-pointer op, barrier) with 2 pthreads
-    as PEs on this host's cores."""
+    as PEs on this host's cores; the pointer is the reference's own compiled
+    shmemu_sum_double_func (src/shmemu/miscops.c, oracle/_ref) when that
+    library is in the tree, else the restated op."""
     import oracle as O
     src = O.team_inputs("double", 2, n, 0x5EED, "unit12")
+    ref = O.ref_elem_fn("double", "sum") is not None
     # size the repetition count for ~10 s of CPU work (bounded sample)
-    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True)
+    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True, ref_ops=ref)
     reps = max(3, min(200, int(10.0 / max(probe, 1e-3))))
     t0 = time.time()
-    sec = O.cpu_baseline("double", "sum", src, reps=reps, pin=True)
+    sec = O.cpu_baseline("double", "sum", src, reps=reps, pin=True, ref_ops=ref)
     wall = time.time() - t0
     B = 2 * 3 * n * 8  # two PE results, each (K+1)*n*8
+    ops = ("the reference's compiled shmemu_sum_double_func (src/shmemu/miscops.c built "
+           "unmodified into oracle/_ref) called by value through a pointer as "
+           "src/reductions.c:95-96 does" if ref else "the restated element op (oracle/_ref absent)")
     out = {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
-           "sample": (f"oracle/oracle_reduce.c reference loop shape, double sum, "
+           "element_ops": "reference" if ref else "restatement",
+           "sample": (f"src/reductions.c:79-113 loop shape restated in oracle/oracle_reduce.c "
+                      f"(copy, barrier, 64-element memcpy getmem chunks, barrier) with {ops}; "
+                      f"double sum, "
                       f"2 PEs (pthreads pinned to the first 2 CPUs this process may use), nreduce={n}, median of "
                       f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
                       f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}, CPUs this "
@@ -119,9 +128,11 @@ def cpu_baseline(n):
     # the same loop with every PE's elements split over 8 threads: 16 cores,
     # this box's CPU share (a one-PE-per-core reference uses 2 for 2 PEs)
     tpp = 8
-    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True, threads_per_pe=tpp)
+    probe = O.cpu_baseline("double", "sum", src, reps=1, pin=True, threads_per_pe=tpp,
+                           ref_ops=ref)
     reps16 = max(3, min(200, int(5.0 / max(probe, 1e-3))))
-    sec16 = O.cpu_baseline("double", "sum", src, reps=reps16, pin=True, threads_per_pe=tpp)
+    sec16 = O.cpu_baseline("double", "sum", src, reps=reps16, pin=True, threads_per_pe=tpp,
+                           ref_ops=ref)
     out["same_loop_16_cores"] = {
         "value": B / sec16 / GIB, "unit": "GiB/s", "cores": 2 * tpp, "ms_per_call": sec16 * 1e3,
         "sample": f"the same loop shape, each PE's elements split over {tpp} pinned threads "
@@ -146,8 +157,10 @@ def cpu_baselines_configs():
     import oracle as O
     out = {"host_nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
            "kind": "port",
-           "note": "oracle/oracle_reduce.c reference loop shape, pthreads pinned to the first P CPUs "
-                   "of this process's CPU set, median after 1 warm-up"}
+           "element_ops": "reference" if O.ref_lib() is not None else "restatement",
+           "note": "oracle/oracle_reduce.c reference loop shape with the reference's compiled "
+                   "element functions (oracle/_ref) when present, pthreads pinned to the first P "
+                   "CPUs of this process's CPU set, median after 1 warm-up"}
     plans = (("config3", "long", ("and", "or", "xor"), 2, 32 << 20, "bits", 3),
              ("config5", "float", ("min", "max", "prod"), 8, 32 << 20, "unit12", 1),
              ("config4", "double", ("sum",), 8, 64 << 20, "unit12", 1))
@@ -157,7 +170,8 @@ def cpu_baselines_configs():
             es = src[0].dtype.itemsize
             res = {"pes": P, "cores": P, "nreduce_sample": n}
             for op in ops:
-                sec = O.cpu_baseline(t, op, src, reps=reps, pin=True)
+                sec = O.cpu_baseline(t, op, src, reps=reps, pin=True,
+                                     ref_ops=O.ref_elem_fn(t, op) is not None)
                 res[op] = {"ms_per_call": sec * 1e3, "GiBs_per_PE": n * es / sec / GIB,
                            "GiBs_fused_convention": P * (P + 1) * n * es / sec / GIB}
             out[name] = res
@@ -494,7 +508,7 @@ def small_call_latency(n=1024, reps=300, sizes=(1024, 4096, 8192, 16384, 32768, 
     for m in sizes:
         src = O.team_inputs("int", 2, m, 5, "bits")
         cpu[m] = O.cpu_baseline("int", "sum", src, reps=max(50, min(2000, int(2e7 / m))),
-                                pin=True) * 1e6
+                                pin=True, ref_ops=O.ref_elem_fn("int", "sum") is not None) * 1e6
     out["cpu_reference_loop_us"] = cpu[n]
     sweep = [{"nreduce": m, "cpu_reference_loop_us": cpu[m],
               "fused_team_us": lat[f"{m}/fused_team"]["us_median"],

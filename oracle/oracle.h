@@ -79,6 +79,12 @@ double oracle_cpu_baseline(int type, int op, int npes,
 double oracle_cpu_baseline_split(int type, int op, int npes,
                                  const void *const *sources, void *const *targets,
                                  int nreduce, int reps, int pin_cores, int tpp);
+/* the same with the reference's own element function (a T (*)(T, T) from
+   oracle/_ref/libref_ops.so, e.g. shmemu_sum_double_func) in the loop;
+   double, float, int and long / long long only */
+double oracle_cpu_baseline_ref(int type, int op, int npes, const void *const *sources,
+                               void *const *targets, int nreduce, int reps, int pin_cores,
+                               int tpp, void *ref_fn);
 
 /*
  * CPU baseline of the data-movement collectives (oracle_coll.c): kind 0

@@ -100,6 +100,8 @@ def lib():
         L.oracle_cpu_baseline.restype = ctypes.c_double
         L.oracle_cpu_baseline_split.argtypes = L.oracle_cpu_baseline.argtypes + [ctypes.c_int]
         L.oracle_cpu_baseline_split.restype = ctypes.c_double
+        L.oracle_cpu_baseline_ref.argtypes = L.oracle_cpu_baseline_split.argtypes + [ctypes.c_void_p]
+        L.oracle_cpu_baseline_ref.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -167,20 +169,41 @@ def fold_with(fn, t, op, sources, me, PE_start, logPE_stride, PE_size):
     return acc
 
 
+def ref_elem_fn(t: str, op: str):
+    """Address of the reference's own compiled element function
+    shmemu_<op>_<t>_func (src/shmemu/miscops.c:12-105, oracle/_ref), or None
+    when oracle/_ref is absent."""
+    R = ref_lib()
+    if R is None:
+        return None
+    try:
+        return ctypes.cast(getattr(R, f"shmemu_{op}_{t}_func"), ctypes.c_void_p).value
+    except AttributeError:
+        return None
+
+
 def cpu_baseline(t: str, op: str, sources: list, reps: int = 5,
-                 pin: bool = True, threads_per_pe: int = 1, targets: list = None) -> float:
+                 pin: bool = True, threads_per_pe: int = 1, targets: list = None,
+                 ref_ops: bool = False) -> float:
     """Median seconds per reduce-to-all call of the reference loop shape,
     one pthread per PE (oracle_reduce.c), or threads_per_pe pthreads per PE
     each running that shape over a contiguous part of the elements.  If
-    `targets` is a list, the PEs' result arrays are appended to it."""
+    `targets` is a list, the PEs' result arrays are appended to it.
+    ref_ops: call the reference's own compiled element function in the loop
+    (oracle/_ref; raises if it is absent)."""
     npes = len(sources)
     srcs = [np.ascontiguousarray(s, dtype=NP_DTYPE[t]) for s in sources]
     tgts = [np.empty_like(srcs[0]) for _ in range(npes)]
     sp = (ctypes.c_void_p * npes)(*[s.ctypes.data for s in srcs])
     tp = (ctypes.c_void_p * npes)(*[x.ctypes.data for x in tgts])
-    sec = lib().oracle_cpu_baseline_split(TYPES.index(t), OPS.index(op), npes, sp, tp,
-                                          srcs[0].size, reps, 1 if pin else 0,
-                                          threads_per_pe)
+    fn = None
+    if ref_ops:
+        fn = ref_elem_fn(t, op)
+        if fn is None:
+            raise ValueError(f"no reference element function for {t}/{op} (oracle/_ref absent?)")
+    sec = lib().oracle_cpu_baseline_ref(TYPES.index(t), OPS.index(op), npes, sp, tp,
+                                        srcs[0].size, reps, 1 if pin else 0,
+                                        threads_per_pe, fn)
     if sec < 0:
         raise ValueError(f"no cpu baseline for {t}/{op}")
     if targets is not None:

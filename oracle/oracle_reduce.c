@@ -23,7 +23,9 @@
  *
  * oracle_cpu_baseline keeps the reference's loop shape instead (pthreads as
  * PEs, memcpy getmem from the peer's slot of an in-process heap, 64-element
- * chunks, per-element call through a function pointer).
+ * chunks, per-element call through a function pointer); with
+ * oracle_cpu_baseline_ref that pointer is the reference's own compiled
+ * element function (oracle/_ref).
  */
 #define _GNU_SOURCE
 #include "oracle.h"
@@ -119,8 +121,21 @@ static elem_fn pick_elem(int type, int op)
     return NULL;
 }
 
+/* The reference's own element function (src/shmemu/miscops.c:12-105,
+   compiled unmodified into oracle/_ref/libref_ops.so), called by value
+   through a pointer exactly as src/reductions.c:95-96 does:
+   write_to[ti] = (*the_op)(write_to[ti], pWrk[j]).  One loop per C type. */
+#define REF_FOLD(T)                                                            \
+    do {                                                                       \
+        T (*f)(T, T) = (T (*)(T, T)) t->ref_fn;                                \
+        T *w = (T *) dst + ti0;                                                \
+        const T *p = (const T *) pw;                                           \
+        for (size_t j = 0; j < cnt; j++) w[j] = (*f)(w[j], p[j]);              \
+    } while (0)
+
 typedef struct {
     int type, npes, nreduce, reps, pin, tpp;  /* tpp: threads per PE */
+    void *ref_fn;                             /* reference element fn, or NULL */
     int *cpus;                                /* thread i pinned to cpus[i] */
     size_t s;
     elem_fn fn;
@@ -189,15 +204,25 @@ static void *bl_pe(void *p)
             if (pe == me) continue;
             const char *peer = (const char *) t->sources[pe] + lo * s; /* same offset */
             size_t ti = 0, si = 0;
-            for (size_t k = 0; k < nloops; k++) {
-                memcpy(pwrk, peer + si * s, WRK * s); /* shmem_getmem :92 */
-                for (int j = 0; j < WRK; j++, ti++)
-                    t->fn(dst + ti * s, pwrk + (size_t) j * s);
-                si += WRK;
+            for (size_t k = 0; k <= nloops; k++) {
+                const size_t cnt = k < nloops ? WRK : nrem;
+                memcpy(pwrk, peer + si * s, cnt * s); /* shmem_getmem :92, :103 */
+                if (t->ref_fn) {                      /* :95-96, the reference's op */
+                    const size_t ti0 = ti;
+                    const char *pw = pwrk;
+                    switch (t->type) {
+                    case OR_DOUBLE: REF_FOLD(double); break;
+                    case OR_FLOAT: REF_FOLD(float); break;
+                    case OR_INT: REF_FOLD(int); break;
+                    default: REF_FOLD(long); break;    /* long, long long */
+                    }
+                    ti += cnt;
+                } else {
+                    for (size_t j = 0; j < cnt; j++, ti++)
+                        t->fn(dst + ti * s, pwrk + j * s);
+                }
+                si += cnt;
             }
-            memcpy(pwrk, peer + si * s, nrem * s);    /* :103 */
-            for (size_t j = 0; j < nrem; j++, ti++)
-                t->fn(dst + ti * s, pwrk + j * s);
         }
         pthread_barrier_wait(&t->bar);                /* :113 */
         if (me == 0 && ar->part == 0) t->times[r] = now_s() - t0;
@@ -214,14 +239,18 @@ static int cmp_d(const void *a, const void *b)
 
 /* the reference loop shape with npes * tpp pthreads (tpp per PE, pinned to
    cores 0 .. npes*tpp-1 when pin_cores); median seconds per call */
-double oracle_cpu_baseline_split(int type, int op, int npes,
-                                 const void *const *sources, void *const *targets,
-                                 int nreduce, int reps, int pin_cores, int tpp)
+double oracle_cpu_baseline_ref(int type, int op, int npes, const void *const *sources,
+                               void *const *targets, int nreduce, int reps, int pin_cores,
+                               int tpp, void *ref_fn)
 {
     elem_fn fn = pick_elem(type, op);
     if (!fn || npes < 1 || reps < 1 || nreduce < 0 || tpp < 1) return -1.0;
+    if (ref_fn && type != OR_DOUBLE && type != OR_FLOAT && type != OR_INT &&
+        type != OR_LONG && type != OR_LONGLONG)
+        return -1.0;
     bl_team t;
     memset(&t, 0, sizeof(t));
+    t.ref_fn = ref_fn;
     t.type = type; t.npes = npes; t.nreduce = nreduce; t.reps = reps; t.pin = pin_cores;
     t.tpp = tpp;
     t.s = oracle_type_size(type); t.fn = fn; t.sources = sources; t.targets = targets;
@@ -248,6 +277,14 @@ double oracle_cpu_baseline_split(int type, int op, int npes,
     free(th);
     free(args);
     return med;
+}
+
+double oracle_cpu_baseline_split(int type, int op, int npes,
+                                 const void *const *sources, void *const *targets,
+                                 int nreduce, int reps, int pin_cores, int tpp)
+{
+    return oracle_cpu_baseline_ref(type, op, npes, sources, targets, nreduce, reps, pin_cores,
+                                   tpp, NULL);
 }
 
 double oracle_cpu_baseline(int type, int op, int npes,

@@ -107,3 +107,13 @@ def test_cpu_baseline_results(t, op, P, tpp):
     for pe in range(P):
         assert np.array_equal(np.asarray(got[pe]).view(np.uint8),
                               np.asarray(want[pe]).view(np.uint8)), pe
+    # the same loop calling the reference's own compiled element function
+    # (oracle/_ref, src/shmemu/miscops.c) through the pointer, as
+    # src/reductions.c:95-96 does -- the form bench.py's cpu_baseline times
+    if O.ref_lib() is not None:
+        got = []
+        O.cpu_baseline(t, op, src, reps=1, pin=False, threads_per_pe=tpp, targets=got,
+                       ref_ops=True)
+        for pe in range(P):
+            assert np.array_equal(np.asarray(got[pe]).view(np.uint8),
+                                  np.asarray(want[pe]).view(np.uint8)), pe
