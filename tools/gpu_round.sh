@@ -48,6 +48,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     multi_tr2) step multi_tr2 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 2 --steps 5 --warmup 2 --deadline 360 ;;
     multi8) step multi8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     teamlayout) step teamlayout 300 python -u tools/team_layout_probe.py && TL_P=2 step teamlayout2 300 python -u tools/team_layout_probe.py && TL_P=8 TL_N=$((32<<20)) step teamlayout8 300 python -u tools/team_layout_probe.py ;;
+    copyvar) step copyvar 600 python -u tools/team_variants.py run_copy ;;
     teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;

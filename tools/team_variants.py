@@ -7,6 +7,9 @@ and 8 members.  Not part of the product.
       tools/variants/<name>/libosgpu_reduce.so, linked with the tree's other
       objects; "git:<rev>" variants take team.hip/combine.hip/elem_ops.hpp
       from that revision (the baseline before a change)
+  python tools/team_variants.py build_copy / run_copy
+      the same for copy.hip (COPY_VARIANTS): the collectives' copy kernel
+      with P ranges of 64 MiB and 512 MiB (osgpu_copy), interleaved rounds
   python tools/team_variants.py run        (on the GPU box)
       every build loaded into one process, interleaved on the same arrays:
       team_vec_kernel through osgpu_team_combine, one launch over n elements
@@ -29,6 +32,10 @@ VARIANTS = {
     "bf": (None, []),
     "bf_u2_2_u8_4": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=4"]),
     "bf_u2_2_u8_4g2": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=2"]),
+}
+COPY_VARIANTS = {
+    "blocked": "git:281a986",   # ranges one after another (before round 3's round-robin)
+    "roundrobin": None,         # the tree's copy.hip
 }
 OTHERS = ["fused.o", "verify.o", "longdouble.o", "copy.o", "runtime.o", "heap.o",
           "shmem_reduce.o", "shmem_collect.o"]
@@ -140,5 +147,77 @@ def run():
             torch.cuda.empty_cache()
 
 
+def build_copy():
+    subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
+    others = ["combine.o", "team.o", "fused.o", "verify.o", "longdouble.o", "runtime.o", "heap.o",
+              "shmem_reduce.o", "shmem_collect.o"]
+    for name, rev in COPY_VARIANTS.items():
+        d = os.path.join(VAR, "copy_" + name)
+        os.makedirs(d, exist_ok=True)
+        src = os.path.join(CSRC, "copy.hip")
+        if rev:
+            src = os.path.join(d, "copy.hip")
+            for f in ("copy.hip", "combine.hpp"):
+                txt = subprocess.run(["git", "show", f"{rev[4:]}:test-resilient-osss-ucx_amd/csrc/{f}"],
+                                     cwd=ROOT, check=True, capture_output=True).stdout
+                open(os.path.join(d, f), "wb").write(txt)
+        subprocess.run(["/opt/rocm/bin/hipcc"] + FL + ["-c", src, "-o", os.path.join(d, "copy.o")],
+                       check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                        os.path.join(d, "libosgpu_reduce.so"), os.path.join(d, "copy.o")] +
+                       [os.path.join(CSRC, o) for o in others] + ["-lrccl", "-ldl", "-lpthread"],
+                       check=True)
+        print("built", name)
+
+
+def run_copy():
+    import ctypes
+    import torch
+    torch.cuda.init()
+    libs = {}
+    for name in COPY_VARIANTS:
+        L = ctypes.CDLL(os.path.join(VAR, "copy_" + name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
+        L.osgpu_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_void_p]
+        libs[name] = L
+    reps = int(os.environ.get("REPS", "10"))
+    rounds = int(os.environ.get("TV_ROUNDS", "7"))
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    for nb in (64 << 20, 512 << 20):
+        for P in (2, 4, 8):
+            src = [torch.empty(nb, dtype=torch.uint8, device="cuda").random_(0, 255) for _ in range(P)]
+            dst = [torch.empty(nb, dtype=torch.uint8, device="cuda") for _ in range(P)]
+            S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in src])
+            D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dst])
+            N = (ctypes.c_size_t * P)(*([nb] * P))
+            torch.cuda.synchronize()
+            times = {name: [] for name in libs}
+            for name, L in libs.items():
+                for _ in range(2):
+                    assert L.osgpu_copy(D, S, N, P, sp) == 0
+            torch.cuda.synchronize()
+            ok = all(torch.equal(a, b) for a, b in zip(src, dst))
+            for _ in range(rounds):
+                for name, L in libs.items():
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(reps):
+                        L.osgpu_copy(D, S, N, P, sp)
+                    e1.record(st)
+                    e1.synchronize()
+                    times[name].append(e0.elapsed_time(e1) * 1e3 / reps)
+            for name in libs:
+                us = sorted(times[name])[len(times[name]) // 2]
+                print(json.dumps({"variant": name, "ranges": P, "bytes_per_range": nb, "us": us,
+                                  "frac": 2 * P * nb / us / 8e6,
+                                  "spread_us": [min(times[name]), max(times[name])],
+                                  "exact": ok}), flush=True)
+            del src, dst
+            torch.cuda.empty_cache()
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    {"build": build, "run": run, "build_copy": build_copy,
+     "run_copy": run_copy}[sys.argv[1]]()
