@@ -426,3 +426,50 @@ def test_team_combine_launcher(torch_cuda, t, op, P, shift):
         assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (t, op, P, q)
         assert (outs[q][:off].cpu().numpy() == 0x5A).all()
         assert (outs[q][off + n * s:].cpu().numpy() == 0x5A).all()
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("sign", [0, 1])
+def test_longdouble_same_sign_sums(torch_cuda, P, sign):
+    """long double sums whose inputs all carry one sign take the
+    addition-only fast add in every round (x87.hpp add_same_fast, a
+    wave-uniform choice per element): whole waves of same-sign elements
+    (wide exponents, carries out of the significand), then the same arrays
+    with a NaN, an infinity and denormals in a few elements -- those lanes'
+    folds leave the fast path while the rest of their wave stays on it.
+    Every member's target bit-exact against the oracle's per-PE fold."""
+    n = 65_537
+    src = O.team_inputs("longdouble", P, n, 0x5A5E + P, "wide")
+    raws = [O.value_bytes(s).reshape(-1, 10).copy() for s in src]
+    for r in raws:
+        r[:, 9] = (r[:, 9] & 0x7F) | (0x80 if sign else 0)
+    for spoil in (False, True):
+        if spoil:   # a few special elements in otherwise same-sign waves
+            k = np.arange(0, n, 997)
+            raws[0][k[::3], :] = 0
+            raws[0][k[::3], 7] = 0xC0       # quiet NaN significand
+            raws[0][k[::3], 8] = 0xFF
+            raws[0][k[::3], 9] = 0x7F | (0x80 if sign else 0)
+            raws[P - 1][k[1::3], :8] = 0
+            raws[P - 1][k[1::3], 7] = 0x80  # infinity: J bit only
+            raws[P - 1][k[1::3], 8] = 0xFF
+            raws[P - 1][k[1::3], 9] = 0x7F | (0x80 if sign else 0)
+            raws[1][k[2::3], 8] = 0         # denormals (exponent 0)
+            raws[1][k[2::3], 9] = 0x80 if sign else 0
+            raws[1][k[2::3], 7] &= 0x7F
+        ins_np = [np.ascontiguousarray(O.from_value_bytes("longdouble", r.reshape(-1)))
+                  for r in raws]
+        want = O.to_all("longdouble", "sum", ins_np)
+        dev = torch_cuda.device("cuda:0")
+        ins = [torch_cuda.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1).copy())
+               .to(dev) for x in ins_np]
+        outs = [torch_cuda.empty(n * 16, dtype=torch_cuda.uint8, device=dev) for _ in range(P)]
+        S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in ins])
+        D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in outs])
+        torch_cuda.cuda.synchronize()
+        L = osgpu.load()
+        assert L.osgpu_team_combine(osgpu.TYPES.index("longdouble"), 0, P, D, S, n, None) == 0
+        torch_cuda.cuda.synchronize()
+        for q in range(P):
+            got = outs[q].cpu().numpy().reshape(-1, 16)[:, :10].reshape(-1)
+            assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (P, sign, spoil, q)
