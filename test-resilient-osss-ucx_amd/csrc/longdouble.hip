@@ -206,8 +206,12 @@ struct LdTeam {
 // in rounds); max / min: team_fold_minmax (P key compares, then every
 // member's pick among the tied extremes).
 // VEC: 16-byte aligned arrays (the x86-64 layout), one dwordx4 per element.
+// At least 4 waves per SIMD (<= 128 VGPRs): the 8-member sum's rounds want
+// 132, and 3 waves per SIMD cost the same-sign sums 6-7 % (interleaved A/B,
+// profiles/r03_ld_variants.jsonl).
 template <int OP, int P, bool VEC>
-__global__ __launch_bounds__(256) void ld_team_kernel(LdTeam a, size_t n)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ld_team_kernel(
+    LdTeam a, size_t n)
 {
     const size_t stride = (size_t) gridDim.x * blockDim.x;
     for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {

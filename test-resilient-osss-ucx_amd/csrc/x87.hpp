@@ -113,12 +113,45 @@ OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s << 15) | x.e}; }
 
 OSGPU_HD inline bool normal_u(XU x) { return x.e - 1u < kEmax - 1u && (x.m >> 63); }
 
+// count of leading zeros of a 32-bit word, ~0 when it is zero (what
+// v_ffbh_u32 returns; clang's ctlz would add a compare and a select)
+OSGPU_HD inline uint32_t ffbh(uint32_t x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t f;
+    asm("v_ffbh_u32 %0, %1" : "=v"(f) : "v"(x));
+    return f;
+#else
+    return x ? (uint32_t) __builtin_clz(x) : ~0u;
+#endif
+}
+
+// |a - b| of two values below 2^16 (one v_sad_u16)
+OSGPU_HD inline uint32_t absdiff15(uint32_t a, uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sad_u16(a, b, 0u);
+#else
+    return a > b ? a - b : b - a;
+#endif
+}
+
+// a - b, 0 when b > a (v_sub_u32 with clamp)
+OSGPU_HD inline uint32_t sub_sat(uint32_t a, uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_sub_sat(a, b);
+#else
+    return b > a ? 0u : a - b;
+#endif
+}
+
 // add of two NORMAL operands (0 < biased exponent < 0x7fff, J set; the
 // caller checks), straight-line: the data-dependent choices (swap, add or
 // subtract, renormalising shift, round up) are selects, so the lanes of a
 // wave -- and several independent folds of one lane -- run one instruction
-// stream.  Returns false where it does not apply: exponent gaps of 64 and 65,
-// cancellation into the low half (exact zero included), results below the
+// stream.  Returns false where it does not apply: exponent gaps of 63 to 65,
+// cancellations of 32 bits or more (exact zero included), results below the
 // normal range or overflowing, a significand of all ones rounded up to the
 // next power of two; add_general then computes the result.
 //
@@ -128,39 +161,63 @@ OSGPU_HD inline bool normal_u(XU x) { return x.e - 1u < kEmax - 1u && (x.m >> 63
 // of leaving the word, and addition and subtraction share one normalising
 // left shift by clz (0 or 1 after an addition).  For d >= 66 B is dropped:
 // it lies below a quarter of A's ulp and RNE returns A.
+//
+// Written for gfx950's issue costs (tools/valu_rate2.hip,
+// profiles/r03_valu_rate2.jsonl): VOP2 and/or/xor/add/sub/lshr/ashr/not/mov
+// issue in ~2.6 cycles per wave64, every compare, select, carry, 64-bit
+// shift, left shift and three-operand op in ~4.5.  So the range flags are
+// two unsigned compares (not ten), B's drop is an arithmetic-shift mask, the
+// shift amounts use the hardware's own masking, the clz of the top word needs
+// no zero test (E saturates instead), and only a cancellation of 32+ bits (gaps of 0 or 1 with 32
+// equal leading bits, ~2^-32 of random operands) leaves the fast path: 52
+// VALU per add against 58 (an estimated 191 issue cycles against 229).
 OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
 {
     const bool swap = b.e > a.e || (b.e == a.e && b.m > a.m);  // |A| >= |B|
     const uint64_t ma = swap ? b.m : a.m;
     uint64_t mb = swap ? a.m : b.m;
-    const uint32_t EA = swap ? b.e : a.e;
-    const uint32_t d = EA - (swap ? a.e : b.e);
+    const uint32_t EA = a.e > b.e ? a.e : b.e;  // the exponents need no select
+    const uint32_t d = absdiff15(a.e, b.e);
     const uint32_t sign = swap ? b.s : a.s;
-    mb = d >= 64 ? 0 : mb;
-    const unsigned sh = d & 63;  // d >= 64: mb == 0
-    const u128 A = ((u128) (ma >> 1) << 64) | (ma << 63);
-    const u128 B = ((u128) ((mb >> sh) >> 1) << 64) | (mb << (63 - sh));
-    // A + B, or A - B as A + ~B + 1, without a data-dependent branch (the
-    // + 1 rides in as the carry into the low word, whose A half is zero)
+    // d >= 63: B dropped -- a mask from the sign of d - 63 (d < 2^15), not a
+    // compare and two selects; gaps of 63..65 are flagged below, so every
+    // shift amount here is the exact gap (0..62) or shifts a zero
+    const uint32_t keep = (uint32_t) ((int32_t) (d - 63u) >> 31);
+    mb &= ((uint64_t) keep << 32) | keep;
+    const uint64_t ah = ma >> 1, bh = mb >> ((d + 1) & 63), bl = mb << ((63 - d) & 63);
+    // S = A + B, or A - B as A + ~B + 1, in 32-bit words with explicit
+    // carries (A's lowest word is 0; the + 1 rides in as the first carry)
     const uint32_t diff = a.s ^ b.s;
-    const uint32_t m32 = 0u - diff;
-    const uint64_t M = ((uint64_t) m32 << 32) | m32;
-    const u128 MM = ((u128) M << 64) | M;
-    const u128 S = A + (B ^ MM) + (u128) diff;
-    uint64_t hi = (uint64_t) (S >> 64), lo = (uint64_t) S;
-    const bool cancel = hi == 0;
-    const int lz = __builtin_clzg(hi, 64);  // 64 only when cancel (flagged)
-    const unsigned l6 = lz & 63;
-    hi = (hi << l6) | ((lo >> 1) >> (63 - l6));
-    lo <<= l6;
-    int E = (int) EA + 1 - lz;
-    const bool low = E < 1;
-    // round to nearest even at bit 64: up when lo > 2^63, or lo == 2^63 and
-    // hi is odd
-    hi += lo > (1ull << 63) - (hi & 1) ? 1 : 0;
-    const bool wrap = hi == 0;  // carried out of 64 bits (all ones rounded up)
-    *r = XU{hi, (uint32_t) E, sign};
-    return d - 64u >= 2u && !cancel && !low && !wrap && E < (int) kEmax;
+    const uint32_t M = 0u - diff;
+    unsigned c0, c1, c2, c3;
+    const uint32_t s0 = __builtin_addc((uint32_t) bl ^ M, 0u, diff, &c0);
+    const uint32_t s1 = __builtin_addc((uint32_t) (bl >> 32) ^ M, (uint32_t) ma << 31, c0, &c1);
+    const uint32_t s2 = __builtin_addc((uint32_t) bh ^ M, (uint32_t) ah, c1, &c2);
+    const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32) ^ M, (uint32_t) (ah >> 32), c2, &c3);
+    (void) c3;
+    // normalise by the leading zeros of the top word: a cancellation of 32
+    // bits or more (top word zero; only for gaps of 0 or 1) gives lz = ~0,
+    // and E saturates to 0 (flagged by the range test; the shifted value is
+    // then not used), so the shift is below 32 and only the top word of the
+    // low half can reach the new high half
+    const uint32_t lz = ffbh(s3);
+    uint64_t hi = ((uint64_t) s3 << 32) | s2, lo = ((uint64_t) s1 << 32) | s0;
+    // (the masks are the hardware's own shift-amount masks: no instruction)
+    hi = (hi << (lz & 63)) | ((s1 >> 1) >> ((31u - lz) & 31));
+    lo <<= lz & 63;
+    const uint32_t E = sub_sat(EA + 1u, lz);  // 0 (flagged) below 1 or for lz = ~0
+    // round to nearest even at bit 64: up iff lo > 2^63 - (hi & 1), i.e. iff
+    // (lo | (hi & 1)) > 2^63; the carry out of hi is the wrap case (all ones
+    // rounded up)
+    const unsigned up = (lo | (hi & 1u)) > (1ull << 63) ? 1u : 0u;
+    unsigned w1, wrap;
+    const uint32_t h0 = __builtin_addc((uint32_t) hi, 0u, up, &w1);
+    const uint32_t hh = __builtin_addc((uint32_t) (hi >> 32), 0u, w1, &wrap);
+    *r = XU{((uint64_t) hh << 32) | h0, E, sign};
+    // not covered: gaps of 63..65, E outside [1, kEmax) (one unsigned range
+    // test; below the normal range, or a cancellation of 32 bits or more,
+    // E is 0), all ones rounded up
+    return d - 63u >= 3u && E - 1u < kEmax - 1u && !wrap;
 }
 
 // add_fast for two NORMAL operands of the SAME sign (the caller checks):
@@ -168,18 +225,19 @@ OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
 // by exponent alone), no complement, and its sum of A = ma * 2^63 and
 // B = mb * 2^(63-d) lies in [2^126, 2^128): the renormalising shift is 0 or
 // 1, a select instead of a clz and three variable funnel shifts.  false:
-// gaps of 64 and 65, overflow, all ones rounded up (add_general computes
-// those).  41 VALU per add against add_fast's 56 (tools/isa/).
+// gaps of 63 to 65, overflow, all ones rounded up (add_general computes
+// those).
 OSGPU_HD inline bool add_same_fast(XU a, XU b, XU *r)
 {
     const bool swap = b.e > a.e;
     const uint64_t ma = swap ? b.m : a.m;
     uint64_t mb = swap ? a.m : b.m;
     const uint32_t EA = swap ? b.e : a.e;
-    const uint32_t d = EA - (swap ? a.e : b.e);
-    mb = d >= 64 ? 0 : mb;
-    const unsigned sh = d & 63;
-    const uint64_t ah = ma >> 1, bh = (mb >> 1) >> sh, bl = mb << (63 - sh);
+    const uint32_t d = absdiff15(a.e, b.e);
+    // d >= 63: B dropped by a mask (add_fast); gaps of 63..65 flagged below
+    const uint32_t keep = (uint32_t) ((int32_t) (d - 63u) >> 31);
+    mb &= ((uint64_t) keep << 32) | keep;
+    const uint64_t ah = ma >> 1, bh = mb >> ((d + 1) & 63), bl = mb << ((63 - d) & 63);
     // S = A + B in 32-bit words with explicit carries; A's lowest word is 0
     unsigned c1, c2, c3;
     const uint32_t s1 = __builtin_addc((uint32_t) (bl >> 32), (uint32_t) ma << 31, 0u, &c1);
@@ -187,21 +245,19 @@ OSGPU_HD inline bool add_same_fast(XU a, XU b, XU *r)
     const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32), (uint32_t) (ah >> 32), c2, &c3);
     (void) c3;  // S < 2^128: no carry out (headroom)
     uint64_t hi = ((uint64_t) s3 << 32) | s2, lo = ((uint64_t) s1 << 32) | (uint32_t) bl;
-    const bool top = (s3 >> 31) != 0;  // S >= 2^127: no shift, else one
-    const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
-    hi = top ? hi : h1;
-    lo = top ? lo : l1;
-    const uint32_t E = EA + (top ? 1u : 0u);  // EA + 1 - lz, lz = !top
-    // round to nearest even at bit 64: up iff lo + 2^63 - 1 + (hi & 1)
-    // carries out of 64 bits (lo > 2^63 - (hi & 1)); the carry out of hi
-    // when it is all ones is the wrap case
-    unsigned u1, up, w1, wrap;
-    (void) __builtin_addc((uint32_t) lo, 0xffffffffu, (unsigned) hi & 1u, &u1);
-    (void) __builtin_addc((uint32_t) (lo >> 32), 0x7fffffffu, u1, &up);
+    // S >= 2^127: no shift, else one -- shifts by t = 1 - top (no selects)
+    const uint32_t top = s3 >> 31, t = top ^ 1u;
+    hi = (hi << t) | ((s1 >> 31) & t);
+    lo <<= t;
+    const uint32_t E = EA + top;  // EA + 1 - lz, lz = t
+    // round to nearest even at bit 64 (add_fast); the carry out of hi when
+    // it is all ones is the wrap case
+    const unsigned up = (lo | (hi & 1u)) > (1ull << 63) ? 1u : 0u;
+    unsigned w1, wrap;
     const uint32_t h0 = __builtin_addc((uint32_t) hi, 0u, up, &w1);
     const uint32_t hh = __builtin_addc((uint32_t) (hi >> 32), 0u, w1, &wrap);
     *r = XU{((uint64_t) hh << 32) | h0, E, a.s};
-    return d - 64u >= 2u && !wrap && E < kEmax;
+    return d - 63u >= 3u && !wrap && E < kEmax;
 }
 
 // true in every lane of the wave (device), or for this element (host, where
@@ -294,12 +350,12 @@ OSGPU_HD inline bool mul_fast(XU a, XU b, XU *r)
 {
     const u128 P = (u128) a.m * (u128) b.m;
     uint64_t hi = (uint64_t) (P >> 64), lo = (uint64_t) P;
-    const bool top = (hi >> 63) != 0;
-    const uint64_t h1 = (hi << 1) | (lo >> 63), l1 = lo << 1;
-    hi = top ? hi : h1;
-    lo = top ? lo : l1;
+    // no shift when P >= 2^127, else one: shifts by t = 1 - top, no selects
+    const uint32_t top = (uint32_t) (hi >> 63), t = top ^ 1u;
+    hi = (hi << t) | ((uint32_t) (lo >> 63) & t);
+    lo <<= t;
     // a.m*2^(Ea-bias-63) * b.m*2^(Eb-bias-63) = S * 2^(E-bias-127)
-    int E = (int) a.e + (int) b.e - kBias + (top ? 1 : 0);
+    int E = (int) a.e + (int) b.e - kBias + (int) top;
     const bool low = E < 1;
     hi += lo > (1ull << 63) - (hi & 1) ? 1 : 0;  // RNE at bit 64 (add_fast)
     const bool wrap = hi == 0;
