@@ -173,7 +173,11 @@ OSGPU_HD inline uint32_t sub_sat(uint32_t a, uint32_t b)
 // VALU per add against 58 (an estimated 191 issue cycles against 229).
 OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
 {
-    const bool swap = b.e > a.e || (b.e == a.e && b.m > a.m);  // |A| >= |B|
+    // |A| >= |B| by one 64-bit compare of (exponent, top significand word);
+    // a tie there (same exponent, same top 32 bits) is flagged below
+    const uint64_t ka = ((uint64_t) a.e << 32) | (uint32_t) (a.m >> 32);
+    const uint64_t kb = ((uint64_t) b.e << 32) | (uint32_t) (b.m >> 32);
+    const bool swap = kb > ka;
     const uint64_t ma = swap ? b.m : a.m;
     uint64_t mb = swap ? a.m : b.m;
     const uint32_t EA = a.e > b.e ? a.e : b.e;  // the exponents need no select
@@ -217,7 +221,7 @@ OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
     // not covered: gaps of 63..65, E outside [1, kEmax) (one unsigned range
     // test; below the normal range, or a cancellation of 32 bits or more,
     // E is 0), all ones rounded up
-    return d - 63u >= 3u && E - 1u < kEmax - 1u && !wrap;
+    return d - 63u >= 3u && E - 1u < kEmax - 1u && !wrap && ka != kb;
 }
 
 // add_fast for two NORMAL operands of the SAME sign (the caller checks):
