@@ -470,6 +470,64 @@ def extra_kernel_rates(L, torch):
         del a, b, o
     torch.cuda.empty_cache()
     out["config3_long_bitwise_256MiB"] = c3
+    try:
+        out["longdouble_team_8_members"] = longdouble_team_rate(L, torch)
+    except Exception as e:  # report, never hide; the fields above stand
+        out["longdouble_team_8_members"] = {"error": repr(e)[:300]}
+    return out
+
+
+def longdouble_team_rate(L, torch, n=4 << 20, P=8, reps=10):
+    """The kernel furthest from the HBM roofline: the x87 soft-float team
+    kernel (csrc/longdouble.hip ld_team_kernel, x87.hpp) for an 8-member
+    long double sum -- every member's own fold order, 49 soft adds per
+    element -- over n elements of 16-B slots, 2*P*n*16 bytes per launch.
+    VALU-bound, so it follows the box's clock.  Data as
+    tools/ld_team_rate.py: random 64-bit significands, exponents
+    2^-3..2^3, random signs (the general fast add in every round) or one
+    sign (the addition-only add)."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5)
+    st = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    dsts_t = [torch.empty((n, 2), dtype=torch.int64, device=dev) for _ in range(P)]
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts_t])
+    B = 2 * P * n * 16
+    out = {"bound": "valu (x87 soft-float; HBM roofline below)", "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "members": P, "nreduce": n, "algorithmic_bytes_per_launch": B,
+           "kernel": f"osgpu::x87::ld_team_kernel<SUM, {P}>"}
+    for dist in ("random_signs", "one_sign"):
+        srcs_t = []
+        for _ in range(P):
+            v = torch.empty((n, 2), dtype=torch.int64, device=dev)
+            v[:, 0] = torch.randint(-(1 << 62), 1 << 62, (n,), device=dev,
+                                    generator=g) | (-(1 << 63))
+            e = 0x3fff + torch.randint(-3, 4, (n,), device=dev, generator=g)
+            sgn = torch.randint(0, 2, (n,), device=dev, generator=g) << 15
+            v[:, 1] = e | (sgn if dist == "random_signs" else 0)
+            srcs_t.append(v)
+        S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs_t])
+        torch.cuda.synchronize()
+
+        def launch():
+            if L.osgpu_team_combine(6, 0, P, D, S, n, sp) != 0:
+                raise RuntimeError(L.osgpu_last_error().decode())
+        for _ in range(3):
+            launch()
+        t = span_per_launch(torch, st, launch, reps)
+        torch.cuda.synchronize()
+        # members 0 and 1 fold x0 + x1 + ... and x1 + x0 + ...: the same bits
+        same01 = bool(torch.equal(dsts_t[0][:, 0], dsts_t[1][:, 0]) and
+                      torch.equal(dsts_t[0][:, 1] & 0xffff, dsts_t[1][:, 1] & 0xffff))
+        out[dist] = {"kernel_avg_us": t * 1e6, "achieved": B / t / 1e9,
+                     "frac": B / t / 1e9 / HBM_PEAK_GBS, "member0_equals_member1": same01}
+        del srcs_t
+    del dsts_t
+    torch.cuda.empty_cache()
+    out["note"] = ("every member's fold order (src/reductions.c:79-111) in x87 80-bit arithmetic "
+                   "(src/shmemu/miscops.c:30); bit-exact against the reference in "
+                   "tests/test_gpu_x87.py; VALU-issue-bound, so the fraction follows the box's "
+                   "clock and power state (0.37-0.51 of 8 TB/s for random signs across boxes, up to 40 % between launches of one run: profiles/r03_ld_team_kernel_stats.csv)")
     return out
 
 
