@@ -86,7 +86,9 @@ _REF = None
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(HERE, "liboracle.so")
+        # ORACLE_LIB: another build of the same sources (tests/test_sanitizers.py
+        # runs the oracle's tests against an ASan/UBSan build)
+        path = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
         if not os.path.exists(path):
             build(ref=False)
         L = ctypes.CDLL(path)

@@ -202,11 +202,15 @@ def build_x87check():
     """The GPU soft-float (csrc/x87.hpp) compiled for the host (test only)."""
     src = os.path.join(HERE, "x87_check.hip")
     hdr = os.path.join(HERE, "..", "..", "test-resilient-osss-ucx_amd", "csrc", "x87.hpp")
-    if (not os.path.exists(X87_PATH)
+    if os.environ.get("X87CHECK_LIB"):   # a sanitizer build (tests/test_sanitizers.py)
+        L = ctypes.CDLL(os.environ["X87CHECK_LIB"])
+    elif (not os.path.exists(X87_PATH)
             or os.path.getmtime(X87_PATH) < max(os.path.getmtime(src), os.path.getmtime(hdr))):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-fPIC", "-shared", "-std=c++17",
                         src, "-o", X87_PATH], check=True, stderr=subprocess.DEVNULL)
-    L = ctypes.CDLL(X87_PATH)
+        L = ctypes.CDLL(X87_PATH)
+    else:
+        L = ctypes.CDLL(X87_PATH)
     L.x87check_op.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_size_t]
     L.x87check_team.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
