@@ -477,7 +477,7 @@ def extra_kernel_rates(L, torch):
     return out
 
 
-def longdouble_team_rate(L, torch, n=4 << 20, P=8, reps=10):
+def longdouble_team_rate(L, torch, n=4 << 20, P=8, reps=20):
     """The kernel furthest from the HBM roofline: the x87 soft-float team
     kernel (csrc/longdouble.hip ld_team_kernel, x87.hpp) for an 8-member
     long double sum -- every member's own fold order, 49 soft adds per
@@ -512,8 +512,15 @@ def longdouble_team_rate(L, torch, n=4 << 20, P=8, reps=10):
         def launch():
             if L.osgpu_team_combine(6, 0, P, D, S, n, sp) != 0:
                 raise RuntimeError(L.osgpu_last_error().decode())
-        for _ in range(3):
-            launch()
+        # warm up by time, not by count: from an idle GPU the first launches
+        # of this power-hungry kernel run while the clock ramps (1.2 ms, then
+        # 0.58-0.63 ms, settling at 0.53 ms for 8 Mi elements;
+        # profiles/r03_clock_probe.jsonl)
+        t_warm = time.time() + 1.5
+        while time.time() < t_warm:
+            for _ in range(20):
+                launch()
+            torch.cuda.synchronize()
         t = span_per_launch(torch, st, launch, reps)
         torch.cuda.synchronize()
         # members 0 and 1 fold x0 + x1 + ... and x1 + x0 + ...: the same bits
@@ -526,8 +533,9 @@ def longdouble_team_rate(L, torch, n=4 << 20, P=8, reps=10):
     torch.cuda.empty_cache()
     out["note"] = ("every member's fold order (src/reductions.c:79-111) in x87 80-bit arithmetic "
                    "(src/shmemu/miscops.c:30); bit-exact against the reference in "
-                   "tests/test_gpu_x87.py; VALU-issue-bound, so the fraction follows the box's "
-                   "clock and power state (0.37-0.51 of 8 TB/s for random signs across boxes, up to 40 % between launches of one run: profiles/r03_ld_team_kernel_stats.csv)")
+                   "tests/test_gpu_x87.py; VALU-issue-bound at ~1360 W and ~2375 MHz in steady state; "
+                   "timed after a 1.5 s warm-up, as from an idle GPU the first launches run "
+                   "while the clock ramps (profiles/r03_clock_probe.jsonl)")
     return out
 
 
