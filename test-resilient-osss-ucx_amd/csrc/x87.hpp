@@ -165,12 +165,14 @@ OSGPU_HD inline uint32_t sub_sat(uint32_t a, uint32_t b)
 // Written for gfx950's issue costs (tools/valu_rate2.hip,
 // profiles/r03_valu_rate2.jsonl): VOP2 and/or/xor/add/sub/lshr/ashr/not/mov
 // issue in ~2.6 cycles per wave64, every compare, select, carry, 64-bit
-// shift, left shift and three-operand op in ~4.5.  So the range flags are
-// two unsigned compares (not ten), B's drop is an arithmetic-shift mask, the
-// shift amounts use the hardware's own masking, the clz of the top word needs
-// no zero test (E saturates instead), and only a cancellation of 32+ bits (gaps of 0 or 1 with 32
-// equal leading bits, ~2^-32 of random operands) leaves the fast path: 52
-// VALU per add against 58 (an estimated 191 issue cycles against 229).
+// shift, left shift and three-operand op in ~4.5.  So the magnitude order is
+// one 64-bit compare of (exponent, top word) with its rare tie flagged, the
+// range flags are two unsigned compares, B's drop is an arithmetic-shift
+// mask, the shift amounts use the hardware's own masking, the exponent gap
+// is one v_sad_u16, and the clz of the top word needs no zero test (E
+// saturates instead): only a cancellation of 32+ bits (gaps of 0 or 1 with
+// 32 equal leading bits, ~2^-32 of random operands) leaves the fast path.
+// 51 VALU per add against 58 (≈ 185 issue cycles against 229).
 OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
 {
     // |A| >= |B| by one 64-bit compare of (exponent, top significand word);
