@@ -45,6 +45,12 @@ struct Inputs {
 
 constexpr int kBlock = 256;
 
+// above 6 inputs: vectors per input in flight per round (U = OSGPU_U_K8 in
+// all); G = U keeps every load of the tile in flight at once
+#ifndef OSGPU_COMBINE_G8
+#define OSGPU_COMBINE_G8 OSGPU_U_K8
+#endif
+
 // lanes per vector-tile unroll: keep K*U*4 VGPRs of payload modest
 template <int K>
 struct Unroll {
@@ -113,17 +119,24 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
     (void) W;
 
     if (tid + (size_t) (U - 1) * kBlock < nvec) {
-        Vec16<T> x[U][K];
+        // the loads of G vectors of every input in flight before their folds
+        // (G = U: all K*U of them; above 6 inputs OSGPU_COMBINE_G8)
+        constexpr int G = K <= 6 ? U : OSGPU_COMBINE_G8;
+        static_assert(G >= 1 && G <= U && U % G == 0, "OSGPU_COMBINE_G8 must divide U");
 #pragma unroll
-        for (int u = 0; u < U; u++)
+        for (int g = 0; g < U; g += G) {
+            Vec16<T> x[G][K];
 #pragma unroll
-            for (int k = 0; k < K; k++)
-                x[u][k].v = __builtin_nontemporal_load(&src[k][tid + (size_t) u * kBlock]);
+            for (int u = 0; u < G; u++)
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            Vec16<T> r;
-            fold_vec<T, OP, K>(x[u], r);
-            __builtin_nontemporal_store(r.v, &dst[tid + (size_t) u * kBlock]);
+                for (int k = 0; k < K; k++)
+                    x[u][k].v = __builtin_nontemporal_load(&src[k][tid + (size_t) (g + u) * kBlock]);
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                Vec16<T> r;
+                fold_vec<T, OP, K>(x[u], r);
+                __builtin_nontemporal_store(r.v, &dst[tid + (size_t) (g + u) * kBlock]);
+            }
         }
     } else {
 #pragma unroll
