@@ -874,7 +874,7 @@ def _block_sums(t, nb, world, torch):
 
 
 def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_bytes, team_ok,
-                    rccl_ok, args, PES):
+                    rccl_ok, args, PES, staging_ok=True):
     """shmem_fcollect64 with one PE per GPU.  Every PE's target gathers all
     contributions: per PE (P-1)/P of the target bytes arrive over xGMI (or
     PCIe for host memory).  Parity: every nb-byte block of every target has
@@ -911,6 +911,9 @@ def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_by
                      "bit_exact_blocks": check(hsrc, htgt, nb)}
     L.osgpu_set_path(osgpu.PATH_AUTO)
 
+    if not staging_ok:
+        out["host_staged_pinned"] = {"skipped": "the staging areas failed their preflight"}
+        return out
     nbh = 64 << 20                                   # host: 64 MiB per PE, pinned
     hs = torch.empty(nbh, dtype=torch.uint8).pin_memory()
     ht = torch.empty(world * nbh, dtype=torch.uint8).pin_memory()
@@ -971,7 +974,7 @@ def _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes, reps=5):
     return out
 
 
-def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
+def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200, flags_ok=True):
     """BASELINE config 1's shape with one PE per GPU: shmem_int_sum_to_all,
     nreduce = 1 Ki, device heaps over xGMI -- host barriers vs the fused
     one-launch path (device-side barriers written across GPUs).  The device
@@ -992,6 +995,9 @@ def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
     L.osgpu_set_device_barrier(2.0, 0)
     try:
         for name, lim in (("host_barriers", 0), ("fused", -1)):
+            if name == "fused" and not flags_ok:
+                out[name] = {"skipped": "the flag areas failed their preflight"}
+                continue
             L.osgpu_set_fused_max_bytes(lim)
             ts, paths, failed = [], set(), False
             for r in range(reps + 10):
@@ -1020,7 +1026,7 @@ def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200):
             if failed:
                 break
     finally:
-        L.osgpu_set_fused_max_bytes(-1)
+        L.osgpu_set_fused_max_bytes(-1 if flags_ok else 0)
         L.osgpu_set_device_barrier(-1, 1)
     return out
 
@@ -1097,6 +1103,17 @@ def bench_multi(args):
                      else "external (torch.distributed.run)",
                      "gpus_visible": ndev, "ranks_per_gpu": -(-world // max(ndev, 1)),
                      "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
+    # which physical GPU every PE runs on (the reference's launcher starts one
+    # PE per slot, src/shmemc/oshrun.in:4): PCI bus id and UUID per rank
+    try:
+        ident = dict(osgpu.device_identity(), rank=rank, local_rank=local)
+    except Exception as e:  # reported, never hidden
+        ident = {"rank": rank, "local_rank": local, "error": repr(e)[:200]}
+    idents = [None] * world
+    dist.all_gather_object(idents, ident)
+    res["launch"]["ranks"] = idents
+    buses = [x.get("pci_bus_id") for x in idents]
+    res["launch"]["distinct_gpus"] = None not in buses and len(set(buses)) == world
     state, emit = start_watchdog(res, rank, args.deadline)
 
     # ---- the device symmetric heap: ONE contiguous virtual range per PE
@@ -1124,17 +1141,24 @@ def bench_multi(args):
     # then copy kernel, BEFORE any kernel uses them (osgpu_preflight); a bad
     # mapping becomes a named entry here instead of a GPU fault later
     state["phase"] = "preflight"
-    staging_ok = True
+    staging_ok = flags_ok = True
     try:
         prc, prep = osgpu.preflight(heap_base, 0, 0, world, psync.value)
         allrep = [None] * world
         dist.all_gather_object(allrep, {"rc": prc, "report": prep})
         res["heap_preflight"] = {str(r): x["report"] for r, x in enumerate(allrep)}
-        heap_bad = any("heap" in str(v.get("status", "")) for x in allrep
-                       for k, v in x["report"].items() if isinstance(v, dict))
-        staging_ok = not any("staging" in str(v.get("status", "")) for x in allrep
-                             for k, v in x["report"].items() if isinstance(v, dict))
+        def failed(region):   # any rank's read or remote-write leg names the region
+            return any(region in str(v.get(leg, ""))
+                       for x in allrep for k, v in x["report"].items() if isinstance(v, dict)
+                       for leg in ("status", "remote_write"))
+        heap_bad = failed("heap")
+        staging_ok = not failed("staging")
+        flags_ok = not failed("flags")
         res["heap_preflight_ok"] = all(x["rc"] == 0 for x in allrep)
+        res["heap_preflight_remote_write"] = (
+            "ok" if all(v.get("remote_write") == "ok" for x in allrep
+                        for k, v in x["report"].items() if isinstance(v, dict))
+            else "failed (heap_preflight)")
         if heap_bad and team_ok:
             # do not run kernels through a mapping that failed its probe
             res["heap_error"] = "preflight: some heap chunk mapping failed (heap_preflight)"
@@ -1142,6 +1166,14 @@ def bench_multi(args):
     except Exception as e:  # report, never hide
         res["heap_preflight"] = {"error": repr(e)[:300]}
         res["heap_preflight_ok"] = False
+        staging_ok = flags_ok = False
+    if not staging_ok:   # the STAGED legs (push exchange, host heaps) would use it
+        res["staging_error"] = ("preflight: a staging-area mapping failed or was not checked; "
+                                "the STAGED and push-exchange legs are skipped")
+    if not flags_ok:     # the fused one-launch path's barriers live in the flag areas
+        res["flags_error"] = ("preflight: a device-barrier flag mapping failed or was not "
+                              "checked; the fused path is off for this run")
+        L.osgpu_set_fused_max_bytes(0)
     _log(rank, f"preflight ok={res.get('heap_preflight_ok')}")
     if team_ok:
         hsrc = osgpu.device_view(heap_base, seg_bytes)
@@ -1152,7 +1184,11 @@ def bench_multi(args):
         res["config"]["heap"] = (f"osgpu_heap_create: {heap_bytes} B contiguous per PE "
                                  f"(VMM chunks, dmabuf)")
     else:
-        res["heap_error"] = vmm_err
+        if vmm_err is not None:
+            res["heap_error"] = vmm_err
+        if heap_base is not None:   # made, but failed its preflight: not used at all
+            L.osgpu_heap_destroy(ctypes.c_void_p(heap_base))
+            heap_base = None
         hsrc = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
         htgt = torch.empty(seg_bytes, dtype=torch.uint8, device=dev)
     src = hsrc[: n * 8].view(torch.float64)
@@ -1230,6 +1266,8 @@ def bench_multi(args):
         # through the owners' inboxes): same bytes on the links
         state["phase"] = "team_push"
         try:
+            if not staging_ok:
+                raise RuntimeError("skipped: the staging areas failed their preflight")
             # full-size identity of the two exchange forms: a position-weighted
             # hash of every PE's whole target (verify.hip), before and after
             h_pull = osgpu.checksum("double", osgpu.CK_HASH, tgt.data_ptr(), n)
@@ -1298,9 +1336,17 @@ def bench_multi(args):
             obj = [bytes(uid)]
             dist.broadcast_object_list(obj, src=0)
             rc = L.osgpu_rccl_init(world, rank, (ctypes.c_char * 128).from_buffer_copy(obj[0]))
+            err = L.osgpu_last_error().decode() if rc != 0 else ""
             rccl_ok = _agree(dist, world, rc == 0)
             if not rccl_ok:
-                raise RuntimeError(L.osgpu_last_error().decode() or "ncclCommInitRank failed")
+                raise RuntimeError(err or "ncclCommInitRank failed on another rank")
+            # the communicator as RCCL sees it: ranks and the device of each
+            nr, ur, cd = osgpu.rccl_comm_info()
+            allc = [None] * world
+            dist.all_gather_object(allc, {"rank": ur, "device": cd,
+                                          "pci_bus_id": ident.get("pci_bus_id")})
+            res["rccl_comm"] = {"nranks": nr, "ranks": allc,
+                                "one_rank_per_gpu": len({c["pci_bus_id"] for c in allc}) == nr}
             L.osgpu_set_path(osgpu.PATH_RCCL)
             t2 = _timed(step, args.steps, args.warmup, dist, torch)
             rr = {"value": args.steps * B / t2 / GIB, "ms_per_step": t2 / args.steps * 1e3,
@@ -1385,7 +1431,10 @@ def bench_multi(args):
             ps = PES.pes_heap(rank) + (1 << 20) - 4096   # symmetric pSync
             g5 = torch.Generator().manual_seed(77 + rank)
             c5 = {"nreduce": n5, "placement": "pinned host memory, STAGED path"}
-            for op, lo, hi in (("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1)):
+            if not staging_ok:
+                c5["skipped"] = "the staging areas failed their preflight"
+            for op, lo, hi in ((("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1))
+                               if staging_ok else ()):
                 h5s.uniform_(lo, hi, generator=g5)
                 f5 = getattr(L, f"shmem_float_{op}_to_all")
 
@@ -1431,7 +1480,8 @@ def bench_multi(args):
         state["phase"] = "collectives"
         try:
             res["collectives"] = _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc,
-                                                 htgt, n * 8, team_ok, rccl_ok, args, PES)
+                                                 htgt, n * 8, team_ok, rccl_ok, args, PES,
+                                                 staging_ok)
             _log(rank, "collectives done")
         except Exception as e:
             res["collectives"] = {"error": repr(e)[:300]}
@@ -1464,7 +1514,8 @@ def bench_multi(args):
     if team_ok and not args.no_extra:
         state["phase"] = "small_calls"
         try:
-            res["small_calls"] = _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES)
+            res["small_calls"] = _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES,
+                                              flags_ok=flags_ok)
             _log(rank, "small calls done")
         except Exception as e:
             res["small_calls"] = {"error": repr(e)[:300]}

@@ -50,6 +50,8 @@ struct CopySeg {
     size_t bytes;
 };
 hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
+// <= 2 KiB of 8-byte words read with plain (L2-cached) loads into dst
+hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t s);
 
 // One-launch reduce-to-all for small calls (fused.hip): the call's two
 // barriers run inside the kernel as epoch flags in every member's flag area

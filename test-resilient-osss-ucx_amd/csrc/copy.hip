@@ -111,7 +111,27 @@ __global__ __launch_bounds__(kThreads) void copy_byte_kernel(SegTable t)
         t.dst[k][i] = t.src[k][i];
 }
 
+// plain (cached) 8-byte loads, one word per lane: the preflight's owner-side
+// read, which first leaves the lines in this GPU's L2 and later re-reads
+// them after peers wrote them remotely (heap.cpp, remote-write leg)
+__global__ __launch_bounds__(kThreads) void probe_load_kernel(const unsigned long long *src,
+                                                              unsigned long long *dst,
+                                                              unsigned words)
+{
+    if (threadIdx.x < words) dst[threadIdx.x] = src[threadIdx.x];
+}
+
 }  // namespace
+
+hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t stream)
+{
+    if (bytes % 8 || bytes / 8 > (size_t) kThreads || ((uintptr_t) src | (uintptr_t) dst) & 7)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(probe_load_kernel, dim3(1), dim3(kThreads), 0, stream,
+                       static_cast<const unsigned long long *>(src),
+                       static_cast<unsigned long long *>(dst), (unsigned) (bytes / 8));
+    return hipGetLastError();
+}
 
 hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t stream)
 {

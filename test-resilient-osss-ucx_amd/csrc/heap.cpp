@@ -719,6 +719,23 @@ extern "C" int osgpu_heap_destroy(void *base)
 // then every member reads every peer's patterns through ITS OWN mapping:
 // first with a host copy (hipMemcpy), then -- only where that matched --
 // with the copy kernel (copy.hip, the code path of the collectives).
+//
+// Then the other direction, the one the team kernel (its stores of shard g
+// into every member's target, team.hip) and the push form (its scatter into
+// the members' staging inboxes) use: remote WRITES into 128 B at both ends
+// of every heap chunk and of the staging area, 16 B per writer (its
+// active-set index).  The owner first reads its blocks with plain cached
+// loads, so the lines sit in its L2; every peer then writes its piece
+// through its mapping -- by host copy, and in a second round by the copy
+// kernel -- and after a barrier the owner re-reads the blocks by kernel and
+// checks every writer's piece.  This is the reference's guarantee that a
+// PE's remote puts are complete and visible at its target before the
+// barrier returns (shmemc_quiet -> ucp_worker_flush ahead of the barrier,
+// src/shmemc/comms.c:147-161, src/shmemc/barrier.c:176-181).
+//
+// Test hook: OSGPU_PREFLIGHT_FAULT=<pe>:<peer> makes PE <pe> reach peer
+// <peer>'s heap chunks and staging through ANOTHER member's mappings (a
+// planted wrong mapping), which both legs must report.
 // ---------------------------------------------------------------------
 
 namespace {
@@ -746,6 +763,26 @@ void pattern(unsigned long long *w, size_t words, int pe, int region, int chunk,
 }
 
 int region_code(const char *r) { return r[0] == 'h' ? 1 : r[0] == 's' ? 2 : 3; }
+
+// the remote-write leg's 16-B piece of `writer` in owner's block
+void wpattern(unsigned long long *w, int writer, int owner, int region, int chunk, int end,
+              int leg)
+{
+    pattern(w, 2, writer, region + 8 * leg, (chunk << 12) ^ owner, end);
+}
+
+// OSGPU_PREFLIGHT_FAULT=<pe>:<peer> (test hook): the active-set index whose
+// mappings PE `me_pe` uses for member index i
+int probe_view(const Coll &c, int me, int i)
+{
+    const char *e = getenv("OSGPU_PREFLIGHT_FAULT");
+    int fpe = -1, fpeer = -1;
+    if (!e || sscanf(e, "%d:%d", &fpe, &fpeer) != 2 || fpe != c.me || fpeer != c.pe_at(i))
+        return i;
+    for (int j = 0; j < c.PE_size; j++)
+        if (j != i && j != me) return j;
+    return me;  // two members: my own range stands in for the peer's
+}
 
 // chunk layout of the heap whose own range starts at `base` (this process)
 bool own_chunks(const char *base, std::vector<size_t> *len)
@@ -781,7 +818,9 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
         for (Heap *h : g_heaps)
             if (h->own.base == (char *) heap_base) H = h;
     }
-    if (heap_base && (!H || H->members.size() != (size_t) PE_size)) {
+    bool same_set = H && H->members.size() == (size_t) PE_size;
+    for (int i = 0; same_set && i < PE_size; i++) same_set = H->members[i] == c.pe_at(i);
+    if (heap_base && !same_set) {
         set_err("%s: %p is not a heap of this active set made by osgpu_heap_create", where,
                 heap_base);
         return OSGPU_EINVAL;  // the same on every member given the same arguments
@@ -817,10 +856,12 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
 
     // 2. the peers' blocks through my mappings
     std::vector<std::vector<Probe>> probes(PE_size);
+    std::vector<std::vector<size_t>> peer_len(PE_size);  // chunk layout of member i's heap
     for (int i = 0; i < PE_size; i++) {
         if (i == me) continue;
+        const int v = probe_view(c, me, i);  // = i unless a fault is planted
         if (H) {
-            std::vector<size_t> len;
+            std::vector<size_t> &len = peer_len[i];
             bool have = false;
             for (const Mapping &m : H->peers)
                 if (m.pe == c.pe_at(i)) {
@@ -828,15 +869,16 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
                     have = true;
                 }
             if (!have) have = own_chunks(H->member_base[i], &len);  // a PE thread here
+            if (!have) len.clear();
             size_t off = 0;
-            for (size_t k = 0; have && k < len.size(); off += len[k], k++) {
-                probes[i].push_back({"heap", (int) k, 0, H->member_base[i] + off, B});
-                probes[i].push_back({"heap", (int) k, 1, H->member_base[i] + off + len[k] - B, B});
+            for (size_t k = 0; k < len.size(); off += len[k], k++) {
+                probes[i].push_back({"heap", (int) k, 0, H->member_base[v] + off, B});
+                probes[i].push_back({"heap", (int) k, 1, H->member_base[v] + off + len[k] - B, B});
             }
         }
         if (S) {
-            probes[i].push_back({"staging", 0, 0, S->region(i), B});
-            probes[i].push_back({"staging", 0, 1, S->region(i) + 4 * S->slot - B, B});
+            probes[i].push_back({"staging", 0, 0, S->region(v), B});
+            probes[i].push_back({"staging", 0, 1, S->region(v) + 4 * S->slot - B, B});
         }
         if (Y) probes[i].push_back({"flags", 0, 0, (const char *) (Y->peer[i] + 31), 8});
     }
@@ -844,12 +886,12 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
     const bool have_tmp = hipMalloc((void **) &dtmp, B) == hipSuccess;
     (void) hipGetLastError();
     hipStream_t st = thread_stream(where);
-    std::string rep = "{";
     bool all = wrote;
     int nprobes = 0, nbad = 0;
+    std::vector<std::string> read_bad(PE_size);
     for (int i = 0; i < PE_size; i++) {
         if (i == me) continue;
-        std::string bad;
+        std::string &bad = read_bad[i];
         for (const Probe &p : probes[i]) {
             nprobes++;
             unsigned long long want[B / 8], got[B / 8];
@@ -877,6 +919,125 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
                 bad += b;
             }
         }
+        all = all && bad.empty();
+    }
+    barrier(c);  // nobody reuses the regions before every member has read them
+
+    // 3. remote writes: 16 B per writer in 128-B blocks at both ends of every
+    // heap chunk and of the staging area (what team.hip's stores into the
+    // members' targets and the push form's inbox scatter do)
+    constexpr size_t WB = 16 * osgpu::kMaxTeam;
+    struct WBlock {
+        const char *region;
+        int chunk, end;
+        char *at;  // the block in member i's memory, as mapped here (mine: my own)
+    };
+    auto blocks_of = [&](int i) {
+        std::vector<WBlock> v;
+        const int m = i == me ? me : probe_view(c, me, i);
+        if (H) {
+            std::vector<size_t> len;
+            if (i == me) len = H->own.len;
+            else len = peer_len[i];
+            char *base = i == me ? H->own.base : H->member_base[m];
+            size_t off = 0;
+            for (size_t k = 0; k < len.size(); off += len[k], k++) {
+                v.push_back({"heap", (int) k, 0, base + off});
+                v.push_back({"heap", (int) k, 1, base + off + len[k] - WB});
+            }
+        }
+        if (S) {
+            char *r = i == me ? S->local : S->region(m);
+            v.push_back({"staging", 0, 0, r});
+            v.push_back({"staging", 0, 1, r + 4 * S->slot - WB});
+        }
+        return v;
+    };
+    const std::vector<WBlock> mine = blocks_of(me);
+    std::vector<std::string> write_bad(PE_size);  // by writer (my view as owner) + my own errors
+    char *wtmp = nullptr;
+    const bool have_wtmp = hipMalloc((void **) &wtmp, WB * 2) == hipSuccess;
+    (void) hipGetLastError();
+    auto note = [&](int i, const WBlock &b, const char *what) {
+        char m[160];
+        snprintf(m, sizeof(m), "%s%s %s%d %s: %s", write_bad[i].empty() ? "" : "; ", b.region,
+                 strcmp(b.region, "heap") ? "" : "chunk ", strcmp(b.region, "heap") ? 0 : b.chunk,
+                 b.end ? "high" : "low", what);
+        write_bad[i] += m;
+    };
+    // the owner's view of its blocks, read by kernel with cached loads
+    auto owner_read = [&](const WBlock &b, unsigned long long *got) {
+        hipError_t e = have_wtmp ? osgpu::launch_probe_load(b.at, wtmp, WB, st) : hipErrorOutOfMemory;
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = hipMemcpy(got, wtmp, WB, hipMemcpyDeviceToHost);
+        (void) hipGetLastError();
+        return e == hipSuccess;
+    };
+    int nwrite = 0, nwbad = 0;
+    if (!mine.empty() || H || S) {
+        // 3a. clear my blocks and pull them into my L2
+        unsigned long long got[WB / 8];
+        for (const WBlock &b : mine) {
+            (void) hipMemset(b.at, 0, WB);
+            (void) hipDeviceSynchronize();
+            (void) owner_read(b, got);
+        }
+        (void) hipGetLastError();
+        barrier(c);
+        for (int leg = 1; leg <= 2; leg++) {
+            // 3b. my piece into every peer's blocks through my mappings
+            for (int i = 0; i < PE_size; i++) {
+                if (i == me) continue;
+                for (const WBlock &b : blocks_of(i)) {
+                    nwrite++;
+                    unsigned long long w[2];
+                    wpattern(w, c.me, c.pe_at(i), region_code(b.region), b.chunk, b.end, leg);
+                    char *at = b.at + 16 * me;
+                    hipError_t e;
+                    if (leg == 1) {
+                        e = hipMemcpy(at, w, 16, hipMemcpyHostToDevice);
+                    } else {  // the copy kernel's 16-B vector store into peer memory
+                        e = have_wtmp ? hipMemcpy(wtmp + WB, w, 16, hipMemcpyHostToDevice)
+                                      : hipErrorOutOfMemory;
+                        osgpu::CopySeg seg = {wtmp + WB, at, 16};
+                        if (e == hipSuccess) e = osgpu::launch_copy(&seg, 1, st);
+                        if (e == hipSuccess) e = hipStreamSynchronize(st);
+                    }
+                    (void) hipGetLastError();
+                    if (e != hipSuccess) {
+                        nwbad++;
+                        note(i, b, leg == 1 ? "host-copy write to the peer failed"
+                                            : "copy-kernel write to the peer failed");
+                    }
+                }
+            }
+            (void) hipDeviceSynchronize();
+            (void) hipGetLastError();
+            barrier(c);  // every writer's stores are complete
+            // 3c. every writer's piece in my blocks, read by kernel
+            for (const WBlock &b : mine) {
+                const bool ok = owner_read(b, got);
+                for (int j = 0; j < PE_size; j++) {
+                    if (j == me) continue;
+                    unsigned long long want[2];
+                    wpattern(want, c.pe_at(j), c.me, region_code(b.region), b.chunk, b.end, leg);
+                    if (!ok || memcmp(got + 2 * j, want, 16)) {
+                        nwbad++;
+                        note(j, b, !ok ? "owner's read kernel failed"
+                                       : leg == 1 ? "its host-copy write not seen by the owner"
+                                                  : "its copy-kernel write not seen by the owner");
+                    }
+                }
+            }
+            barrier(c);  // the owners have read this round before the next one writes
+        }
+    }
+    if (have_wtmp) (void) hipFree(wtmp);
+    if (have_tmp) (void) hipFree(dtmp);
+
+    std::string rep = "{";
+    for (int i = 0; i < PE_size; i++) {
+        if (i == me) continue;
         char b[96];
         int nheap = 0;
         for (const Probe &p : probes[i]) nheap += !strcmp(p.region, "heap") && p.end == 0;
@@ -884,13 +1045,14 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
                  rep.size() > 1 ? ", " : "", c.pe_at(i), nheap, S ? "true" : "false",
                  Y ? "true" : "false");
         rep += b;
-        rep += bad.empty() ? "\"status\": \"ok\"}" : "\"status\": \"" + bad + "\"}";
-        all = all && bad.empty();
+        rep += read_bad[i].empty() ? "\"status\": \"ok\", " : "\"status\": \"" + read_bad[i] + "\", ";
+        rep += write_bad[i].empty() ? "\"remote_write\": \"ok\"}"
+                                    : "\"remote_write\": \"" + write_bad[i] + "\"}";
+        all = all && write_bad[i].empty();
     }
     rep += "}";
-    if (have_tmp) (void) hipFree(dtmp);
-    barrier(c);  // nobody reuses the regions before every member has read them
-    DBG("%s PE %d: %d probes, %d bad", where, c.me, nprobes, nbad);
+    DBG("%s PE %d: %d probes, %d bad; %d remote writes, %d bad", where, c.me, nprobes, nbad,
+        nwrite, nwbad);
     if (report) {
         if (rep.size() + 1 > report_bytes) {
             set_err("%s: the report needs %zu bytes", where, rep.size() + 1);
@@ -900,6 +1062,8 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
         memcpy(report, rep.c_str(), rep.size() + 1);
     }
     if (!wrote) set_err("%s: writing this PE's patterns failed", where);
-    else if (!all) set_err("%s: %d of %d probes failed", where, nbad, nprobes);
+    else if (!all)
+        set_err("%s: %d of %d read probes and %d remote-write checks failed", where, nbad, nprobes,
+                nwbad);
     return all ? OSGPU_OK : OSGPU_EPEER;
 }

@@ -1032,6 +1032,51 @@ int osgpu_rccl_init(int npes, int me, const void *uid)
     return OSGPU_OK;
 }
 
+int osgpu_rccl_comm_info(int *nranks, int *rank, int *device)
+{
+    if (!g_rccl.world) {
+        set_err("osgpu_rccl_comm_info: no communicator (osgpu_rccl_init)");
+        return OSGPU_EINVAL;
+    }
+    int n = -1, r = -1, d = -1;
+    ncclResult_t e = ncclCommCount(g_rccl.world, &n);
+    if (e == ncclSuccess) e = ncclCommUserRank(g_rccl.world, &r);
+    if (e == ncclSuccess) e = ncclCommCuDevice(g_rccl.world, &d);
+    if (e != ncclSuccess) {
+        set_err("ncclCommCount / UserRank / CuDevice: %s", ncclGetErrorString(e));
+        return OSGPU_ERCCL;
+    }
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+    if (device) *device = d;
+    return OSGPU_OK;
+}
+
+int osgpu_device_identity(char *out, size_t out_bytes)
+{
+    int d = -1;
+    hipError_t e = hipGetDevice(&d);
+    char bus[64] = {0};
+    if (e == hipSuccess) e = hipDeviceGetPCIBusId(bus, (int) sizeof(bus) - 1, d);
+    hipUUID u;
+    if (e == hipSuccess) e = hipDeviceGetUuid(&u, d);
+    if (e != hipSuccess) {
+        set_err("osgpu_device_identity: %s", hipGetErrorString(e));
+        (void) hipGetLastError();
+        return OSGPU_EHIP;
+    }
+    char hex[2 * sizeof(u.bytes) + 1];
+    for (size_t i = 0; i < sizeof(u.bytes); i++)
+        snprintf(hex + 2 * i, 3, "%02x", (unsigned) (unsigned char) u.bytes[i]);
+    const int need = snprintf(out, out_bytes, "{\"device\": %d, \"pci_bus_id\": \"%s\", \"uuid\": \"%s\"}",
+                              d, bus, hex);
+    if (need < 0 || (size_t) need >= out_bytes) {
+        set_err("osgpu_device_identity: the report needs %d bytes", need + 1);
+        return OSGPU_EINVAL;
+    }
+    return OSGPU_OK;
+}
+
 int osgpu_rccl_finalize(void)
 {
     if (!g_rccl.world) return OSGPU_OK;

@@ -55,6 +55,20 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_G8
 #define OSGPU_TEAM_G8 2
 #endif
+// the register-heavy folds above 4 members (complex products: 4-6 VALU
+// temporaries per element per output) take rounds of OSGPU_TEAM_GH vectors
+#ifndef OSGPU_TEAM_GH
+#define OSGPU_TEAM_GH 2
+#endif
+// 1: above 4 members, round r+1's loads are issued before round r's folds
+// and stores (two round buffers), so a lane's loads stay in flight while
+// it stores; 0: round after round
+#ifndef OSGPU_TEAM_PIPE
+#define OSGPU_TEAM_PIPE 0
+#endif
+#ifndef OSGPU_TEAM_PEROUT
+#define OSGPU_TEAM_PEROUT 0
+#endif
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
 // the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
 // (same interleaved A/B)
@@ -64,6 +78,36 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_U4
 #define OSGPU_TEAM_U4 OSGPU_U_K4
 #endif
+
+// Launch shape per (T, OP, P): U vectors per input per lane in rounds of G
+template <typename T, int OP, int P>
+struct TeamShape {
+    static constexpr bool kHeavy = (std::is_same<T, cfloat>::value || std::is_same<T, cdouble>::value) &&
+                                   OP == OP_PROD;
+    static constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
+    static constexpr int G = P <= 4 ? U : (kHeavy ? OSGPU_TEAM_GH : OSGPU_TEAM_G8);
+    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1;
+    // ordered folds above 4 members: fold, check and store one output at a
+    // time instead of all P outputs, then all P stores
+    static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
+    // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
+    // round reads and writes past the tile (and past nvec)
+    static_assert(G >= 1 && G <= U && U % G == 0, "the round size must divide U");
+};
+
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction
+// (a #pragma unroll on the round loop is dropped for the largest bodies)
+template <int I, int N>
+struct Rounds {
+    template <typename F>
+    __device__ __forceinline__ static void run(F &&f)
+    {
+        if constexpr (I < N) {
+            f(std::integral_constant<int, I>{});
+            Rounds<I + 1, N>::run(f);
+        }
+    }
+};
 
 // E: Elem<T, OP> (exact) or Fast<T, OP> (branch-free, elem_ops.hpp)
 template <typename T, int OP, int P, bool ORDERED, typename E = Elem<T, OP>>
@@ -93,7 +137,8 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                                                               int nedge)
 {
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
+    using S = TeamShape<T, OP, P>;
+    constexpr int U = S::U;
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -110,6 +155,36 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
     // the tile's loads stay in flight ahead of the folds
     using F = Fast<T, OP>;
     auto fold_store = [&](TVec<T> (&in)[P], size_t j) {
+        if constexpr (ORDERED && S::kPerOutput) {
+            // one output at a time: fold, check, store -- only one output
+            // vector live beside the inputs
+            Rounds<0, P>::run([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                TVec<T> out;
+                bool bad = false;
+#pragma unroll
+                for (int w = 0; w < W; w++) {
+                    T acc = in[q].e[w];
+#pragma unroll
+                    for (int k = 0; k < P; k++)
+                        if (k != q) acc = F::f(acc, in[k].e[w]);
+                    out.e[w] = acc;
+                    bad = bad || F::bad(acc);
+                }
+                if (F::kChecked && __builtin_expect(bad, 0)) {
+#pragma unroll
+                    for (int w = 0; w < W; w++) {
+                        T acc = in[q].e[w];
+#pragma unroll
+                        for (int k = 0; k < P; k++)
+                            if (k != q) acc = Elem<T, OP>::f(acc, in[k].e[w]);
+                        out.e[w] = acc;
+                    }
+                }
+                __builtin_nontemporal_store(out.v, reinterpret_cast<u32x4 *>(a.dst[q] + head) + j);
+            });
+            return;
+        }
         TVec<T> out[P];
         bool bad = false;
 #pragma unroll
@@ -143,23 +218,38 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         // whole tile: the loads of G vectors of every input are in flight
         // before the first fold, as in combine_vec_kernel -- P*G*16 B per
         // lane, not P*16 B per round trip.  G = U up to 4 inputs; above,
-        // OSGPU_TEAM_G8 (all 4*P at once spills the 8-input complex sum)
-        constexpr int G = P <= 4 ? U : OSGPU_TEAM_G8;
-        // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
-        // round reads and writes past the tile (and past nvec)
-        static_assert(G >= 1 && G <= U && U % G == 0, "OSGPU_TEAM_G8 must divide OSGPU_TEAM_U8");
-#pragma unroll
-        for (int g = 0; g < U; g += G) {
-            TVec<T> in[G][P];
+        // TeamShape's G (all 4*P at once spills the 8-input complex sum)
+        constexpr int G = S::G;
+        constexpr int R = U / G;
+        auto load_round = [&](TVec<T> (&in)[G][P], int g) {
 #pragma unroll
             for (int u = 0; u < G; u++)
 #pragma unroll
                 for (int p = 0; p < P; p++)
                     in[u][p].v = __builtin_nontemporal_load(
                         reinterpret_cast<const u32x4 *>(a.src[p] + head) + t0 +
-                        (size_t) (g + u) * kTeamBlock);
+                        (size_t) (g * G + u) * kTeamBlock);
+        };
+        if constexpr (S::kPipe) {
+            // round r+1's loads go out before round r's stores
+            TVec<T> b0[G][P], b1[G][P];
+            load_round(b0, 0);
+            Rounds<0, R>::run([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                auto &cur = (r % 2 == 0) ? b0 : b1;
+                auto &nxt = (r % 2 == 0) ? b1 : b0;
+                if constexpr (r + 1 < R) load_round(nxt, r + 1);
 #pragma unroll
-            for (int u = 0; u < G; u++) fold_store(in[u], t0 + (size_t) (g + u) * kTeamBlock);
+                for (int u = 0; u < G; u++) fold_store(cur[u], t0 + (size_t) (r * G + u) * kTeamBlock);
+            });
+        } else {
+            Rounds<0, R>::run([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                TVec<T> in[G][P];
+                load_round(in, r);
+#pragma unroll
+                for (int u = 0; u < G; u++) fold_store(in[u], t0 + (size_t) (r * G + u) * kTeamBlock);
+            });
         }
         return;
     }
@@ -214,7 +304,7 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
+    constexpr int U = TeamShape<T, OP, P>::U;
     size_t head = phase ? (16 - phase) / sizeof(T) : 0;
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;

@@ -122,6 +122,8 @@ def load() -> ctypes.CDLL:
     L.osgpu_ipc_close.argtypes = [vp]
     L.osgpu_rccl_unique_id.argtypes = [vp]
     L.osgpu_rccl_init.argtypes = [i, i, vp]
+    L.osgpu_rccl_comm_info.argtypes = [ctypes.POINTER(i)] * 3
+    L.osgpu_device_identity.argtypes = [ctypes.c_char_p, sz]
     L.osgpu_set_path.argtypes = [i]
     L.osgpu_set_stream.argtypes = [vp]
     L.osgpu_get_stream.restype = vp
@@ -217,7 +219,7 @@ def preflight(heap_base, PE_start: int, logPE_stride: int, PE_size: int, psync: 
     """osgpu_preflight (collective): (status code, per-peer report dict)."""
     import json
     L = load()
-    buf = ctypes.create_string_buffer(1 << 16)
+    buf = ctypes.create_string_buffer(1 << 20)
     rc = L.osgpu_preflight(heap_base, PE_start, logPE_stride, PE_size, psync, buf, len(buf))
     try:
         rep = json.loads(buf.value.decode() or "{}")
@@ -226,6 +228,27 @@ def preflight(heap_base, PE_start: int, logPE_stride: int, PE_size: int, psync: 
     if rc != 0:
         rep["error"] = L.osgpu_last_error().decode()
     return rc, rep
+
+
+def rccl_comm_info():
+    """(nranks, rank, device) of the RCCL communicator (ncclCommCount /
+    ncclCommUserRank / ncclCommCuDevice); raises without one."""
+    L = load()
+    v = [ctypes.c_int(-1) for _ in range(3)]
+    rc = L.osgpu_rccl_comm_info(*[ctypes.byref(x) for x in v])
+    if rc != 0:
+        raise RuntimeError(L.osgpu_last_error().decode())
+    return tuple(x.value for x in v)
+
+
+def device_identity() -> dict:
+    """The calling thread's current device: {"device", "pci_bus_id", "uuid"}."""
+    import json
+    L = load()
+    buf = ctypes.create_string_buffer(256)
+    if L.osgpu_device_identity(buf, len(buf)) != 0:
+        raise RuntimeError(L.osgpu_last_error().decode())
+    return json.loads(buf.value.decode())
 
 
 def last_path() -> str:

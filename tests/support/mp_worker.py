@@ -248,9 +248,16 @@ def preflight_mode(L, PES, rank, world):
     exact = bool(np.array_equal(out_t.cpu().numpy(), want))
     ran = osgpu.last_path()
     dist.barrier()
+    # a planted wrong mapping (heap.cpp test hook): PE 0 reaches PE 1's heap
+    # chunks and staging through PE 2's ranges
+    os.environ["OSGPU_PREFLIGHT_FAULT"] = "0:1"
+    rc_fault, rep_fault = osgpu.preflight(base, 0, 0, world, psync)
+    del os.environ["OSGPU_PREFLIGHT_FAULT"]
+    dist.barrier()
     assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
     return {"preflight_rc": rc, "preflight": rep, "preflight_none_rc": rc_none,
-            "preflight_none": rep_none, "after_exact": exact, "after_path": ran}
+            "preflight_none": rep_none, "after_exact": exact, "after_path": ran,
+            "fault_rc": rc_fault, "fault": rep_fault}
 
 
 def mixed_topology_mode(L, rank, world):

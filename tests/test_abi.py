@@ -60,6 +60,75 @@ def test_header_compiles_as_c_and_cxx(tmp_path):
                     "-o", str(tmp_path / "b.o")], check=True)
 
 
+REF_INCLUDE = "/root/reference/include"
+
+
+def _ref_pin_source(lang):
+    """One translation unit holding the reference's own declarations
+    (include/shmem.h -> shmem/api.h:2173-2409, the pshmem_ declarations of
+    include/pshmem.h:745-935, COMPLEXIFY include/shmem/defs.h:14-19) and
+    then ours: a signature that
+    differs from the reference's is a conflicting declaration of the same
+    extern "C" function, a compile error in C11 and in C++17.  Every one of
+    the 88 reduce-to-all names (and the collectives both headers declare)
+    is then taken as a pointer of the REFERENCE's declared type."""
+    names = [n for n in osgpu.header_symbols()
+             if n.endswith("_to_all") or any(k in n for k in ("broadcast", "collect", "alltoall"))]
+    if lang == "c":
+        body = "".join(f"  {{ __typeof__(&{n}) p = &{n}; sink((void (*)(void)) p); }}\n"
+                       for n in names)
+        pre = "static void sink(void (*p)(void)) { (void) p; }\n"
+    else:
+        body = "".join(f"  {{ decltype(&::{n}) p = &::{n}; sink(reinterpret_cast<void (*)()>(p)); }}\n"
+                       for n in names)
+        pre = "static void sink(void (*p)()) { (void) p; }\n"
+    # include/pshmem.h does not compile on its own (int32 / int64 / uint32
+    # at :695-699 are undeclared anywhere), so its declarations of the
+    # reduce-to-all and fcollect names are read out of it at test time
+    import re
+    ptext = open(os.path.join(REF_INCLUDE, "pshmem.h")).read()
+    pdecl = re.findall(r"void\s+pshmem_\w+(?:_to_all|broadcast\d+|collect\d+|alltoall\d+)\s*"
+                       r"\([^;]*\);", ptext)
+    assert len([d for d in pdecl if "_to_all" in d]) == 44
+    psect = ('#ifdef __cplusplus\nextern "C" {\n#endif\n' + "\n".join(pdecl) +
+             '\n#ifdef __cplusplus\n}\n#endif\n')
+    return ('#include <shmem.h>\n' + psect + '#include "osgpu_reduce.h"\n' + pre +
+            "int main(void) {\n" + body + "  return 0;\n}\n"), names
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INCLUDE), reason="reference checkout absent")
+@pytest.mark.parametrize("lang", ["c", "cxx"])
+def test_header_matches_reference_header(tmp_path, lang):
+    """include/osgpu_reduce.h against the reference's include/shmem.h and
+    include/pshmem.h's declarations in one translation unit, -Wall -Werror; a planted
+    signature change (nreduce int -> long in one entry point) fails it."""
+    src, names = _ref_pin_source(lang)
+    assert len([n for n in names if n.endswith("_to_all")]) == 88
+    ext, cc, std = (".c", "gcc", "-std=c11") if lang == "c" else (".cpp", "g++", "-std=c++17")
+    f = tmp_path / ("pin" + ext)
+    f.write_text(src)
+
+    def compile_with(inc):
+        return subprocess.run([cc, std, "-Wall", "-Werror", "-c", str(f), "-I", REF_INCLUDE,
+                               "-I", inc, "-o", str(tmp_path / "pin.o")],
+                              capture_output=True, text=True)
+    r = compile_with(os.path.join(ROOT, "include"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    # planted: shmem_int_sum_to_all with a long nreduce
+    planted = tmp_path / "planted"
+    planted.mkdir()
+    hdr = open(os.path.join(ROOT, "include", "osgpu_reduce.h")).read()
+    marker = "OSGPU_DECL_ALL(shmem_)\n"
+    assert marker in hdr
+    hdr = hdr.replace(marker, marker + "void shmem_int_sum_to_all(int *target, int *source, long "
+                      "nreduce, int PE_start, int logPE_stride, int PE_size, int *pWrk, "
+                      "long *pSync);\n")
+    (planted / "osgpu_reduce.h").write_text(hdr)
+    r = compile_with(str(planted))
+    assert r.returncode != 0
+    assert "shmem_int_sum_to_all" in r.stderr
+
+
 def test_link_a_c_program_against_the_library(tmp_path):
     """A C application links the drop-in exactly like the reference's
     libshmem (no GPU call happens: nreduce = 0 only synchronises)."""

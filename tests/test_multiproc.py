@@ -395,7 +395,11 @@ def test_preflight_processes(tmp_path, monkeypatch):
     """osgpu_preflight with 3 processes on cuda:0 over a heap of three
     64-MiB chunks: every chunk end, staging area and flag word of every peer
     reads back its owner's pattern through this process's mapping (host copy
-    and copy kernel); a reduction on the same heap afterwards is bit-exact."""
+    and copy kernel), and every peer's remote writes into this process's
+    chunk ends and staging area (host copy, then copy kernel) reach it; a
+    reduction on the same heap afterwards is bit-exact.  A planted wrong
+    mapping (OSGPU_PREFLIGHT_FAULT=0:1: PE 0 reaches PE 1 through PE 2's
+    ranges) fails PE 0's reads of PE 1 and PE 1's check of PE 0's writes."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -409,10 +413,21 @@ def test_preflight_processes(tmp_path, monkeypatch):
         assert peers == sorted(str(p) for p in range(world) if p != r), x["preflight"]
         for p in peers:
             e = x["preflight"][p]
-            assert e == {"chunks": 3, "staging": True, "flags": True, "status": "ok"}, (r, p, e)
+            assert e == {"chunks": 3, "staging": True, "flags": True, "status": "ok",
+                         "remote_write": "ok"}, (r, p, e)
             f = x["preflight_none"][p]
             assert f["chunks"] == 0 and f["staging"] and f["status"] == "ok", (r, p, f)
+            assert f["remote_write"] == "ok", (r, p, f)
         assert x["after_exact"] and x["after_path"] == "team", x
+    # the planted fault: PE 0's reads of PE 1 read PE 2's data; PE 1 never
+    # sees PE 0's writes (they went to PE 2); both calls fail
+    f0, f1 = res[0]["fault"], res[1]["fault"]
+    assert res[0]["fault_rc"] != 0 and res[1]["fault_rc"] != 0, (f0, f1)
+    assert "read other data" in f0["1"]["status"], f0
+    assert f0["2"]["status"] == "ok", f0
+    rw = f1["0"]["remote_write"]
+    assert "not seen by the owner" in rw and "heap chunk 2 high" in rw and "staging" in rw, f1
+    assert f1["2"]["remote_write"] == "ok", f1
 
 
 @pytest.mark.gpu

@@ -50,6 +50,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     teamlayout) step teamlayout 300 python -u tools/team_layout_probe.py && TL_P=2 step teamlayout2 300 python -u tools/team_layout_probe.py && TL_P=8 TL_N=$((32<<20)) step teamlayout8 300 python -u tools/team_layout_probe.py ;;
     copyvar) step copyvar 600 python -u tools/team_variants.py run_copy ;;
     teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
+    sweep) step sweep 900 python -u tools/team_variants.py run_sweep ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;

@@ -19,20 +19,29 @@ and 8 members.  Not part of the product.
 """
 import json
 import os
+import shutil
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc")
 VAR = os.path.join(ROOT, "tools", "variants")
+VARLIB = os.path.join(ROOT, "tools", "varlib")
 FL = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
       "-fno-fast-math"]
 VARIANTS = {
-    "base": ("git:HEAD", []),
-    "bf": (None, []),
-    "bf_u2_2_u8_4": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=4"]),
-    "bf_u2_2_u8_4g2": (None, ["-DOSGPU_TEAM_U2=2", "-DOSGPU_TEAM_U8=4", "-DOSGPU_TEAM_G8=2"]),
+    "r03": ("git:5c84853", []),                       # round 3's shipped team kernel
+    "tree": (None, []),                               # the tree's defaults
+    "pipe": (None, ["-DOSGPU_TEAM_PIPE=1"]),
+    "gh1": (None, ["-DOSGPU_TEAM_GH=1"]),
+    "pipe_g1": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_G8=1", "-DOSGPU_TEAM_GH=1"]),
+    "perout": (None, ["-DOSGPU_TEAM_PEROUT=1"]),
+    "pipe_perout": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_PEROUT=1"]),
+    "u8_pipe_g2": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_U8=8", "-DOSGPU_TEAM_G8=2",
+                          "-DOSGPU_TEAM_GH=1"]),
 }
+if os.environ.get("TV_BUILD"):
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["TV_BUILD"].split(",")}
 COPY_VARIANTS = {
     "blocked": "git:281a986",   # ranges one after another (before round 3's round-robin)
     "roundrobin": None,         # the tree's copy.hip
@@ -56,16 +65,30 @@ def build():
                                      cwd=ROOT, check=True, capture_output=True).stdout
                 open(os.path.join(src, f), "wb").write(txt)
         for f in ("team", "combine"):
+            tmp = os.path.join(d, "tmp_" + f)
+            os.makedirs(tmp, exist_ok=True)
             procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + FL + flags +
-                                          ["-c", os.path.join(src, f + ".hip"), "-o",
-                                           os.path.join(d, f + ".o")]))
+                                          ["--save-temps", "-c", os.path.join(src, f + ".hip"),
+                                           "-o", os.path.join(d, f + ".o")], cwd=tmp))
     assert all(p.wait() == 0 for p in procs)
+    for name in VARIANTS:   # register table of every team kernel (tools/isa/reg_table.py)
+        d = os.path.join(VAR, name)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa", "reg_table.py"),
+                        os.path.join(d, "tmp_team", "team-hip-amdgcn-amd-amdhsa-gfx950.s"),
+                        "team_vec_kernel", "--json", os.path.join(d, "regs.jsonl")],
+                       check=True, capture_output=True)
     for name in VARIANTS:
         d = os.path.join(VAR, name)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                         os.path.join(d, "libosgpu_reduce.so"), os.path.join(d, "team.o"),
                         os.path.join(d, "combine.o")] + [os.path.join(CSRC, o) for o in OTHERS] +
                        ["-lrccl", "-ldl", "-lpthread"], check=True)
+        # tools/variants/ stays here (.gpurunignore: the save-temps are
+        # hundreds of MB); the library and its register table travel
+        lib = os.path.join(VARLIB, name)
+        os.makedirs(lib, exist_ok=True)
+        for f in ("libosgpu_reduce.so", "regs.jsonl"):
+            shutil.copy(os.path.join(d, f), lib)
         print("built", name)
 
 
@@ -81,7 +104,7 @@ def run():
     names = os.environ.get("TV_NAMES", ",".join(VARIANTS)).split(",")
     libs = {}
     for name in names:
-        L = ctypes.CDLL(os.path.join(VAR, name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
+        L = ctypes.CDLL(os.path.join(VARLIB, name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
         L.osgpu_team_combine.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         libs[name] = L
@@ -145,6 +168,110 @@ def run():
                                   "member0_exact": exact[name]}), flush=True)
             del xs, ys, acc
             torch.cuda.empty_cache()
+
+
+def run_sweep():
+    """Every (type, op) at every P in TV_PS, every variant library in
+    TV_NAMES loaded into one process and interleaved round by round with
+    the same-mix copy ceiling (osgpu_copy: P ranges of n*s bytes in one
+    launch, the copy kernel's round-robin tiles -- P read and P write streams
+    over the same bytes, nothing folded).  Inputs: products in [0.9, 1.1)
+    (no overflow over 8 factors), sums in [-1.5, 1.5), min/max in
+    [-1e3, 1e3), integers random bits; no NaN.  Every variant's P outputs
+    are compared byte for byte with the first variant's.  One JSON line per
+    (type, op, P, variant) on stdout and in gpurun_out/team_sweep.jsonl."""
+    import ctypes
+    import torch
+    torch.cuda.init()
+    names = os.environ.get("TV_NAMES", ",".join(VARIANTS)).split(",")
+    libs = {}
+    for name in names:
+        L = ctypes.CDLL(os.path.join(VARLIB, name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
+        L.osgpu_team_combine.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.osgpu_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_void_p]
+        libs[name] = L
+    C = libs[names[0]]
+    reps = int(os.environ.get("REPS", "5"))
+    rounds = int(os.environ.get("TV_ROUNDS", "5"))
+    nbytes = int(os.environ.get("TV_BYTES", str(512 << 20)))
+    PS = [int(p) for p in os.environ.get("TV_PS", "2,4,5,6,7,8").split(",")]
+    types = {"short": (0, 2, "i"), "int": (1, 4, "i"), "long": (2, 8, "i"), "float": (4, 4, "f"),
+             "double": (5, 8, "d"), "complexf": (7, 8, "f"), "complexd": (8, 16, "d")}
+    ops = {"sum": 0, "prod": 1, "and": 2, "or": 3, "xor": 4, "max": 5, "min": 6}
+    only = os.environ.get("TV_TYPES")
+    only_ops = os.environ.get("TV_OPS")
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    srcs = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(8)]
+    dsts = {k: [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(8)]
+            for k in ("first", "other")}
+    g = torch.Generator(device="cuda").manual_seed(17)
+    outf = open(os.path.join(ROOT, "gpurun_out", "team_sweep.jsonl"), "a")
+    for t, (code, es, kind) in types.items():
+        if only and t not in only.split(","):
+            continue
+        n = nbytes // es
+        for op, oc in ops.items():
+            if kind != "i" and op in ("and", "or", "xor"):
+                continue
+            if t.startswith("complex") and op in ("max", "min"):
+                continue
+            if only_ops and op not in only_ops.split(","):
+                continue
+            for b in srcs:
+                if kind == "i":
+                    b.view(torch.int32).random_(generator=g)
+                else:
+                    v = b.view(torch.float32 if kind == "f" else torch.float64)
+                    lo, hi = {"prod": (0.9, 1.1), "sum": (-1.5, 1.5)}.get(op, (-1e3, 1e3))
+                    v.uniform_(lo, hi, generator=g)
+            for P in PS:
+                S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs[:P]])
+                # variants 2.. write into the second output set (compared
+                # with the first variant's after their first launches)
+                D0 = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts["first"][:P]])
+                D1 = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts["other"][:P]])
+                N = (ctypes.c_size_t * P)(*([n * es] * P))
+                torch.cuda.synchronize()
+                equal = {}
+                for i, name in enumerate(names):
+                    D = D0 if i == 0 else D1
+                    for _ in range(2):
+                        assert libs[name].osgpu_team_combine(code, oc, P, D, S, n, sp) == 0
+                    st.synchronize()
+                    if i > 0:
+                        equal[name] = all(torch.equal(dsts["first"][q], dsts["other"][q])
+                                          for q in range(P))
+                for _ in range(2):
+                    assert C.osgpu_copy(D1, S, N, P, sp) == 0
+                times = {name: [] for name in names + ["copy"]}
+                for _ in range(rounds):
+                    for name in names + ["copy"]:
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(st)
+                        for _ in range(reps):
+                            if name == "copy":
+                                C.osgpu_copy(D1, S, N, P, sp)
+                            else:
+                                libs[name].osgpu_team_combine(code, oc, P, D1, S, n, sp)
+                        e1.record(st)
+                        e1.synchronize()
+                        times[name].append(e0.elapsed_time(e1) * 1e3 / reps)
+                B = 2 * P * n * es
+                cus = sorted(times["copy"])[rounds // 2]
+                for name in names:
+                    us = sorted(times[name])[rounds // 2]
+                    rec = {"type": t, "op": op, "P": P, "variant": name, "n": n, "us": us,
+                           "frac": B / us / 8e6, "copy_us": cus, "copy_frac": B / cus / 8e6,
+                           "frac_of_copy": cus / us,
+                           "spread_us": [min(times[name]), max(times[name])],
+                           "equal_to_" + names[0]: equal.get(name, True)}
+                    print(json.dumps(rec), flush=True)
+                    outf.write(json.dumps(rec) + "\n")
+                outf.flush()
 
 
 def build_copy():
@@ -219,5 +346,5 @@ def run_copy():
 
 
 if __name__ == "__main__":
-    {"build": build, "run": run, "build_copy": build_copy,
+    {"build": build, "run": run, "run_sweep": run_sweep, "build_copy": build_copy,
      "run_copy": run_copy}[sys.argv[1]]()
