@@ -147,6 +147,12 @@ __device__ __forceinline__ int gate_wait(const FusedArgs &a, int word)
 // set: the host continues the call with resume = 1).
 __device__ __forceinline__ bool entry_gate(const FusedArgs &a, int &s_go)
 {
+    if (gridDim.x == 1) {  // the decider is the whole grid: no gate word round trip
+        if (threadIdx.x == 0)
+            s_go = wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1);
+        __syncthreads();
+        return s_go;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0)
         gate_set(a, kFlagGateIn, wait_epoch(a.mine + kFlagArrive, a.P, a.epoch, a.timeout, a.err, 1));
     if (threadIdx.x == 0) s_go = gate_wait(a, kFlagGateIn);

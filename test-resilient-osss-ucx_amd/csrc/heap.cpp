@@ -336,9 +336,12 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
 
     // A kept heap of this member set at least this size, if every member has
     // one from the same creation: register its first `total` bytes again
-    // instead of making a new one (the smallest that fits, so a job that
-    // alternates sizes holds at most its largest heap per member set).  The
-    // candidate must be THIS PE's: PE threads of one process share the pool.
+    // instead of making a new one (the smallest that fits).  A kept heap
+    // never serves a LARGER request, and its HBM is not returned: a job
+    // holds, per member set, the sum of every heap size that exceeded all
+    // the set's earlier heaps (4, then 8, then 16 GiB keeps 28 GiB) -- make
+    // the largest heap first and later ones fit inside it.  The candidate
+    // must be THIS PE's: PE threads of one process share the pool.
     HeapMsg *mine = reinterpret_cast<HeapMsg *>(pSync + kHeapPsync);
     Heap *cand = nullptr;
     {

@@ -133,19 +133,99 @@ void entry_order(const char *where, hipStream_t st)
     entry_sync(where, st);
 }
 
-// Completion of our own stream: hipStreamSynchronize (default; measured
-// 11.8 us launch-to-return for an empty kernel against 13.5 us polling
-// hipStreamQuery, profiles/r01_overhead_probe.jsonl) or poll (OSGPU_SYNC=spin).
+// Completion of our own stream.  OSGPU_SYNC:
+//   block (default)  hipStreamSynchronize (11.8 us launch-to-return for an
+//                    empty kernel, profiles/r01_overhead_probe.jsonl);
+//   spin             poll hipStreamQuery (13.5 us);
+//   word             hipStreamWriteValue64 of a sequence number into a
+//                    host-mapped word behind the stream's work, the host
+//                    spinning on that word (an empty kernel's host-visible
+//                    word: 6.4 us); hipStreamQuery every 64 K spins turns a
+//                    faulted stream into an error instead of a hang.
+// OSGPU_CALL_TRACE=1: host clock at each phase of a host-barrier call
+// (run_team), printed on stderr by PE 0 as "[osgpu call] <phase> <us> ..."
+void call_trace(int me, int phase, const char *label)
+{
+    static const bool on = getenv("OSGPU_CALL_TRACE") != nullptr;
+    if (!on || me != 0) return;
+    thread_local std::chrono::steady_clock::time_point t[8];
+    thread_local const char *names[8];
+    thread_local int n = 0;
+    if (phase == 0) n = 0;
+    if (n < 8) {
+        t[n] = std::chrono::steady_clock::now();
+        names[n++] = label;
+    }
+    if (!strcmp(label, "end")) {
+        std::string out = "[osgpu call]";
+        for (int i = 1; i < n; i++) {
+            char b[64];
+            snprintf(b, sizeof(b), " %s %.2f", names[i],
+                     std::chrono::duration<double, std::micro>(t[i] - t[i - 1]).count());
+            out += b;
+        }
+        fprintf(stderr, "%s us\n", out.c_str());
+    }
+}
+
+int sync_mode()
+{
+    static const int m = [] {
+        const char *e = getenv("OSGPU_SYNC");
+        if (e && !strcmp(e, "spin")) return 1;
+        if (e && !strcmp(e, "word")) return 2;
+        return 0;
+    }();
+    return m;
+}
+
+struct DoneWord {
+    volatile unsigned long long *h = nullptr;
+    void *d = nullptr;
+    unsigned long long seq = 0;
+    int device = -1;
+};
+thread_local DoneWord t_done;
+
 void stream_wait(const char *where, hipStream_t st)
 {
-    static const int spin = env_choice("OSGPU_SYNC", "spin", 0);
-    if (!spin) {
+    const int mode = sync_mode();
+    if (mode == 0) {
         HIPCHK(where, hipStreamSynchronize(st));
         return;
     }
     hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
-    if (e != hipSuccess) fatal(where, "stream: %s", hipGetErrorString(e));
+    if (mode == 1) {
+        while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+        if (e != hipSuccess) fatal(where, "stream: %s", hipGetErrorString(e));
+        return;
+    }
+    int dev = 0;
+    HIPCHK(where, hipGetDevice(&dev));
+    if (!t_done.h || t_done.device != dev) {  // one word per thread and device
+        void *h = nullptr;
+        HIPCHK(where, hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(where, hipHostGetDevicePointer(&t_done.d, h, 0));
+        t_done.h = static_cast<volatile unsigned long long *>(h);
+        *t_done.h = 0;
+        t_done.seq = 0;
+        t_done.device = dev;
+    }
+    const unsigned long long want = ++t_done.seq;
+    HIPCHK(where, hipStreamWriteValue64(st, t_done.d, want, 0));
+    for (unsigned long spins = 1;; spins++) {
+        if (*t_done.h >= want) return;
+        __builtin_ia32_pause();
+        if ((spins & 0xffff) == 0) {
+            e = hipStreamQuery(st);
+            if (e == hipSuccess) {  // the write is behind everything: it must show
+                for (int k = 0; k < 1000000 && *t_done.h < want; k++) __builtin_ia32_pause();
+                if (*t_done.h >= want) return;
+                fatal(where, "stream idle but its completion word was not written");
+            }
+            if (e != hipErrorNotReady) fatal(where, "stream: %s", hipGetErrorString(e));
+        }
+    }
 }
 
 // --------------------------------------------------------------- type info

@@ -53,6 +53,7 @@ int entry_mode();
 void entry_sync(const char *where, hipStream_t own = nullptr);
 void entry_order(const char *where, hipStream_t st);
 void stream_wait(const char *where, hipStream_t st);
+void call_trace(int me, int phase, const char *label);
 
 // --------------------------------------------------------------- type info
 

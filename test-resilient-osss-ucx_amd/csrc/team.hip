@@ -60,14 +60,25 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_GH
 #define OSGPU_TEAM_GH 2
 #endif
-// 1: above 4 members, round r+1's loads are issued before round r's folds
-// and stores (two round buffers), so a lane's loads stay in flight while
-// it stores; 0: round after round
+// 1: above 4 members, integer folds issue round r+1's loads before round
+// r's folds and stores (two round buffers), so a lane's loads stay in
+// flight while it stores; 0: round after round.  Integers only: for every
+// floating-point fold the two buffers cost 0.2-0.4 of the rate (the
+// compiler no longer keeps a round's loads in flight), against +0.5-1 % for
+// the integer ones (profiles/r04_team_type_op_sweep.jsonl)
 #ifndef OSGPU_TEAM_PIPE
-#define OSGPU_TEAM_PIPE 0
+#define OSGPU_TEAM_PIPE 1
 #endif
 #ifndef OSGPU_TEAM_PEROUT
-#define OSGPU_TEAM_PEROUT 0
+#define OSGPU_TEAM_PEROUT 1
+#endif
+// from this many members on: the LDS-staged kernel (team_lds_kernel), one
+// wave per member, 16-B vectors per lane per tile OSGPU_TEAM_LDS_U
+#ifndef OSGPU_TEAM_LDS_MIN_P
+#define OSGPU_TEAM_LDS_MIN_P 9
+#endif
+#ifndef OSGPU_TEAM_LDS_U
+#define OSGPU_TEAM_LDS_U 4
 #endif
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
 // the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
@@ -86,10 +97,11 @@ struct TeamShape {
                                    OP == OP_PROD;
     static constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
     static constexpr int G = P <= 4 ? U : (kHeavy ? OSGPU_TEAM_GH : OSGPU_TEAM_G8);
-    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1;
+    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1 && std::is_integral<T>::value;
     // ordered folds above 4 members: fold, check and store one output at a
     // time instead of all P outputs, then all P stores
     static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
+    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P;
     // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
     // round reads and writes past the tile (and past nvec)
     static_assert(G >= 1 && G <= U && U % G == 0, "the round size must divide U");
@@ -267,6 +279,93 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
     }
 }
 
+// x[k] of a compile-time-sized array at a wave-uniform runtime index
+template <typename X, int P>
+__device__ __forceinline__ X pick(const X (&x)[P], int k)
+{
+    X r = x[0];
+#pragma unroll
+    for (int p = 1; p < P; p++)
+        if (k == p) r = x[p];
+    return r;
+}
+
+// LDS-staged form: P waves per workgroup, a tile of 64*U 16-B vectors of
+// every member.  Wave p streams member p's source tile into LDS (one read
+// stream per wave, as the copy kernel); after the barrier wave q folds the
+// tile of all P inputs from LDS in member q's order and streams member q's
+// target tile (one write stream per wave).  HBM bytes as the register form
+// (2*P*s per element); the LDS carries P reads of every staged byte.
+template <typename T, int OP, int P, bool ORDERED, int U>
+__global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size_t nvec,
+                                                          size_t head, size_t tail_start,
+                                                          int nedge)
+{
+    constexpr int W = 16 / sizeof(T);
+    constexpr int V = 64 * U;  // vectors per member per tile
+    __shared__ u32x4 tile[P][V];
+    if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
+        const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
+        T x[P], r[P];
+#pragma unroll
+        for (int p = 0; p < P; p++) x[p] = a.src[p][e];
+        team_fold<T, OP, P, ORDERED>(x, r);
+#pragma unroll
+        for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
+    }
+    const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
+    const int lane = (int) (threadIdx.x & 63);
+    const size_t base = (size_t) blockIdx.x * V;
+    const bool whole = base + V <= nvec;
+    {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(pick(a.src, w) + head) + base;
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (whole || base + u * 64 + lane < nvec)
+                v[u] = __builtin_nontemporal_load(src + u * 64 + lane);
+#pragma unroll
+        for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
+    }
+    __syncthreads();
+    using F = Fast<T, OP>;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(pick(a.dst, w) + head) + base;
+    // member q's fold of element e: x[q] first, then the others ascending
+    // (order-independent integer ops: ascending for every q)
+    Rounds<0, P>::run([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (w != q) return;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!whole && base + u * 64 + lane >= nvec) continue;
+            TVec<T> in[P], out;
+#pragma unroll
+            for (int p = 0; p < P; p++) in[p].v = tile[p][u * 64 + lane];
+            bool bad = false;
+#pragma unroll
+            for (int e = 0; e < W; e++) {
+                T acc = in[ORDERED ? q : 0].e[e];
+#pragma unroll
+                for (int k = 0; k < P; k++)
+                    if (k != (ORDERED ? q : 0)) acc = F::f(acc, in[k].e[e]);
+                out.e[e] = acc;
+                bad = bad || F::bad(acc);
+            }
+            if (F::kChecked && __builtin_expect(bad, 0)) {
+#pragma unroll
+                for (int e = 0; e < W; e++) {
+                    T acc = in[q].e[e];
+#pragma unroll
+                    for (int k = 0; k < P; k++)
+                        if (k != q) acc = Elem<T, OP>::f(acc, in[k].e[e]);
+                    out.e[e] = acc;
+                }
+            }
+            __builtin_nontemporal_store(out.v, dst + u * 64 + lane);
+        }
+    });
+}
+
 template <typename T, int OP, int P, bool ORDERED>
 __global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> a, size_t n)
 {
@@ -310,6 +409,14 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
     const size_t nvec = (n - head) / W;
     const size_t tail_start = head + nvec * W;
     const int nedge = (int) (head + (n - tail_start));
+    if constexpr (TeamShape<T, OP, P>::kLds) {
+        constexpr int UL = OSGPU_TEAM_LDS_U;
+        size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
+        if (blocks == 0) blocks = 1;
+        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
+                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge);
+        return hipGetLastError();
+    }
     size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),

@@ -21,7 +21,7 @@ import pytest
 
 import oracle as O
 import osgpu
-from test_x87_softfloat import _pairs, raw_random
+from test_x87_softfloat import _deep_cancel_pairs, _pairs, raw_random
 
 pytestmark = pytest.mark.gpu
 
@@ -82,6 +82,16 @@ def test_device_cancellation(torch_cuda):
 @pytest.mark.parametrize("where", ["unit", "underflow", "overflow"])
 def test_device_aligned_operand_boundaries(torch_cuda, where):
     a, b = _pairs(where)
+    _check(torch_cuda, a, b)
+    _check(torch_cuda, b, a)
+
+
+@pytest.mark.parametrize("gap", [0, 1])
+def test_device_deep_cancellation_top_word(torch_cuda, gap):
+    """add_fast's normalisation for every leading-zero count of the top word
+    (opposite signs, gaps 0 and 1, top words k apart, k up to 2^25) on the
+    device build, both operand orders."""
+    a, b = _deep_cancel_pairs(gap)
     _check(torch_cuda, a, b)
     _check(torch_cuda, b, a)
 

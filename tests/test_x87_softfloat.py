@@ -117,6 +117,57 @@ def _pairs(where, n=60_000):
     return pack(ma, ea, sa), pack(mb, eb, sb)
 
 
+def _deep_cancel_pairs(gap, n=120_000, seed=41):
+    """Opposite-sign normal pairs near 1 whose difference cancels 7 to 31
+    leading bits of the top significand word (x87.hpp add_fast's normalise
+    by ffbh of the top word and its funnel shift, every lz in 0..31):
+    gap 0: b's top 32-bit significand word = a's +- k; gap 1: a's top word
+    0x80000000 against b's 0xFFFFFFFF - k (2a - b is then about k * 2^32);
+    k = 2^j + a random part below 2^j for j in 0..24 (k in 1..2^25), the low
+    words random."""
+    r = O.splitmix64(seed + gap, 5 * n).reshape(5, n)
+    j = (r[0] % np.uint64(25)).astype(np.uint64)
+    k = (np.uint64(1) << j) + (r[1] & ((np.uint64(1) << j) - np.uint64(1)))
+    top = np.uint64(1 << 31)
+    if gap == 0:
+        ta = top + (r[2] >> np.uint64(33)) % (np.uint64(1 << 31) - np.uint64(1 << 26)) \
+            + np.uint64(1 << 25)
+        up = (r[3] & np.uint64(1)).astype(bool)
+        tb = np.where(up, ta + k, ta - k)
+        tb = np.minimum(tb, np.uint64(0xFFFFFFFF))
+    else:
+        ta = np.full(n, top, np.uint64)
+        tb = np.uint64(0xFFFFFFFF) - k + np.uint64(1)
+    ma = (ta << np.uint64(32)) | (r[3] >> np.uint64(32))
+    mb = (tb << np.uint64(32)) | (r[4] & np.uint64(0xFFFFFFFF))
+    ea = np.full(n, 16383, np.uint64) + (r[2] & np.uint64(3)) - np.uint64(1)
+    eb = ea - np.uint64(gap)
+    sa = (r[4] >> np.uint64(40)) & np.uint64(1)
+    sb = sa ^ np.uint64(1)
+
+    def pack(m, e, sg):
+        arr = np.zeros((n, 16), np.uint8)
+        arr[:, :8] = m.astype(np.uint64).view(np.uint8).reshape(n, 8)
+        arr[:, 8:10] = (e | (sg << np.uint64(15))).astype(np.uint16).view(np.uint8).reshape(n, 2)
+        return arr.reshape(-1).view(np.longdouble)
+    return pack(ma, ea, sa), pack(mb, eb, sb)
+
+
+@pytest.mark.parametrize("gap", [0, 1])
+def test_deep_cancellation_top_word(x87, gap):
+    """add_fast's normalisation for every leading-zero count of the top
+    word (only small lz were reached before): opposite signs,
+    exponent gaps 0 and 1, top significand words k apart for k up to 2^25,
+    both operand orders, bit-exact against the host's x87."""
+    a, b = _deep_cancel_pairs(gap)
+    raw = (O.value_bytes(a).reshape(-1, 10)[:, 4:8].copy().view(np.uint32).reshape(-1).astype(np.int64)
+           - O.value_bytes(b).reshape(-1, 10)[:, 4:8].copy().view(np.uint32).reshape(-1).astype(np.int64))
+    if gap == 0:   # the top words really differ by 1 .. 2^25
+        assert (np.abs(raw) >= 1).all() and (np.abs(raw) <= 1 << 25).all()
+    check(x87, a, b, use_ref=O.ref_lib() is not None)
+    check(x87, b, a, use_ref=O.ref_lib() is not None)
+
+
 @pytest.mark.parametrize("where", ["unit", "underflow", "overflow"])
 def test_aligned_operand_boundaries(x87, where):
     """The normal-operand fast path of x87 add (x87.hpp add_fast): exponent

@@ -31,14 +31,18 @@ FL = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"
       "-fno-fast-math"]
 VARIANTS = {
     "r03": ("git:5c84853", []),                       # round 3's shipped team kernel
-    "tree": (None, []),                               # the tree's defaults
-    "pipe": (None, ["-DOSGPU_TEAM_PIPE=1"]),
-    "gh1": (None, ["-DOSGPU_TEAM_GH=1"]),
-    "pipe_g1": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_G8=1", "-DOSGPU_TEAM_GH=1"]),
-    "perout": (None, ["-DOSGPU_TEAM_PEROUT=1"]),
-    "pipe_perout": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_PEROUT=1"]),
+    "tree": (None, ["-DOSGPU_TEAM_PIPE=0", "-DOSGPU_TEAM_PEROUT=0"]),  # r04 shape, r03 order
+    "gh1": (None, ["-DOSGPU_TEAM_GH=1", "-DOSGPU_TEAM_PIPE=0", "-DOSGPU_TEAM_PEROUT=0"]),
+    "pipe_g1": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_G8=1", "-DOSGPU_TEAM_GH=1",
+                       "-DOSGPU_TEAM_PEROUT=0"]),
+    "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
+    "tree2": (None, []),                              # round 4: per-output folds, integer pipeline
+    "lds5": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5"]),
+    "lds2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=2"]),
+    "lds5u2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5", "-DOSGPU_TEAM_LDS_U=2"]),
+    "lds5u8": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5", "-DOSGPU_TEAM_LDS_U=8"]),
     "u8_pipe_g2": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_U8=8", "-DOSGPU_TEAM_G8=2",
-                          "-DOSGPU_TEAM_GH=1"]),
+                          "-DOSGPU_TEAM_GH=1", "-DOSGPU_TEAM_PEROUT=0"]),
 }
 if os.environ.get("TV_BUILD"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["TV_BUILD"].split(",")}
