@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "combine.hpp"
@@ -73,12 +74,29 @@ constexpr int kTeamBlock = 256;
 #define OSGPU_TEAM_PEROUT 1
 #endif
 // from this many members on: the LDS-staged kernel (team_lds_kernel), one
-// wave per member, 16-B vectors per lane per tile OSGPU_TEAM_LDS_U
+// wave per member, 16-B vectors per lane per tile OSGPU_TEAM_LDS_U (below 8
+// members) and OSGPU_TEAM_LDS_U8 (8).  On a box whose copy kernel moved
+// 0.76 of 8 TB/s at 8 ranges it reached 0.938 of that copy against 0.898
+// for the register form at 8 members, 0.96-1.04 against 0.91-0.95 at 5-7;
+// 8 vectors per lane (64 KiB of LDS per workgroup at 8 members) fell to
+// 0.44-0.62 (profiles/r04_team_sweep_2.jsonl).  On another box U = 4 beat
+// U = 2 at 3-8 members (1.01-1.02 against 0.95-0.97 of the copy at 5-7,
+// r04_team_sweep_3.jsonl); the complex double product at 8 members stays
+// on the register form there (0.90 against 0.76-0.89 staged)
 #ifndef OSGPU_TEAM_LDS_MIN_P
-#define OSGPU_TEAM_LDS_MIN_P 9
+#define OSGPU_TEAM_LDS_MIN_P 3
 #endif
 #ifndef OSGPU_TEAM_LDS_U
 #define OSGPU_TEAM_LDS_U 4
+#endif
+#ifndef OSGPU_TEAM_LDS_U8
+#define OSGPU_TEAM_LDS_U8 4
+#endif
+// 1: the LDS form as a persistent grid (workgroups resident at once per
+// CU x CUs) walking tiles, two LDS tile buffers: a wave's loads of its next
+// tile are in flight while it folds and stores this one
+#ifndef OSGPU_TEAM_LDS_PERSIST
+#define OSGPU_TEAM_LDS_PERSIST 0
 #endif
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
 // the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
@@ -101,7 +119,9 @@ struct TeamShape {
     // ordered folds above 4 members: fold, check and store one output at a
     // time instead of all P outputs, then all P stores
     static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
-    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P;
+    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P &&
+                                 !(std::is_same<T, cdouble>::value && OP == OP_PROD && P >= 8);
+    static constexpr int kLdsU = P >= 8 ? OSGPU_TEAM_LDS_U8 : OSGPU_TEAM_LDS_U;
     // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
     // round reads and writes past the tile (and past nvec)
     static_assert(G >= 1 && G <= U && U % G == 0, "the round size must divide U");
@@ -296,14 +316,20 @@ __device__ __forceinline__ X pick(const X (&x)[P], int k)
 // tile of all P inputs from LDS in member q's order and streams member q's
 // target tile (one write stream per wave).  HBM bytes as the register form
 // (2*P*s per element); the LDS carries P reads of every staged byte.
-template <typename T, int OP, int P, bool ORDERED, int U>
+// PERSIST: the grid walks the tiles (tile t, t + gridDim.x, ...) with two
+// LDS buffers; a wave's loads of its next tile are issued right after the
+// barrier, so they are in flight while it folds and stores this one (the
+// barrier of the next tile orders every wave's reads of a buffer before
+// anyone overwrites it two tiles later).
+template <typename T, int OP, int P, bool ORDERED, int U, bool PERSIST>
 __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                           size_t head, size_t tail_start,
                                                           int nedge)
 {
     constexpr int W = 16 / sizeof(T);
     constexpr int V = 64 * U;  // vectors per member per tile
-    __shared__ u32x4 tile[P][V];
+    constexpr int NB = PERSIST ? 2 : 1;
+    __shared__ u32x4 tile[NB][P][V];
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -315,55 +341,74 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
     }
     const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
     const int lane = (int) (threadIdx.x & 63);
-    const size_t base = (size_t) blockIdx.x * V;
-    const bool whole = base + V <= nvec;
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(pick(a.src, w) + head) + base;
-        u32x4 v[U];
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(pick(a.src, w) + head);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(pick(a.dst, w) + head);
+    u32x4 v[U];
+    auto load = [&](size_t t) {
+        const size_t base = t * V;
+        const bool whole = base + V <= nvec;
 #pragma unroll
         for (int u = 0; u < U; u++)
             if (whole || base + u * 64 + lane < nvec)
-                v[u] = __builtin_nontemporal_load(src + u * 64 + lane);
-#pragma unroll
-        for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
-    }
-    __syncthreads();
+                v[u] = __builtin_nontemporal_load(src + base + u * 64 + lane);
+    };
     using F = Fast<T, OP>;
-    u32x4 *dst = reinterpret_cast<u32x4 *>(pick(a.dst, w) + head) + base;
     // member q's fold of element e: x[q] first, then the others ascending
     // (order-independent integer ops: ascending for every q)
-    Rounds<0, P>::run([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        if (w != q) return;
+    auto fold_store = [&](int b, size_t t) {
+        const size_t base = t * V;
+        const bool whole = base + V <= nvec;
+        Rounds<0, P>::run([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (w != q) return;
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (!whole && base + u * 64 + lane >= nvec) continue;
-            TVec<T> in[P], out;
+            for (int u = 0; u < U; u++) {
+                if (!whole && base + u * 64 + lane >= nvec) continue;
+                TVec<T> in[P], out;
 #pragma unroll
-            for (int p = 0; p < P; p++) in[p].v = tile[p][u * 64 + lane];
-            bool bad = false;
-#pragma unroll
-            for (int e = 0; e < W; e++) {
-                T acc = in[ORDERED ? q : 0].e[e];
-#pragma unroll
-                for (int k = 0; k < P; k++)
-                    if (k != (ORDERED ? q : 0)) acc = F::f(acc, in[k].e[e]);
-                out.e[e] = acc;
-                bad = bad || F::bad(acc);
-            }
-            if (F::kChecked && __builtin_expect(bad, 0)) {
+                for (int p = 0; p < P; p++) in[p].v = tile[b][p][u * 64 + lane];
+                bool bad = false;
 #pragma unroll
                 for (int e = 0; e < W; e++) {
-                    T acc = in[q].e[e];
+                    T acc = in[ORDERED ? q : 0].e[e];
 #pragma unroll
                     for (int k = 0; k < P; k++)
-                        if (k != q) acc = Elem<T, OP>::f(acc, in[k].e[e]);
+                        if (k != (ORDERED ? q : 0)) acc = F::f(acc, in[k].e[e]);
                     out.e[e] = acc;
+                    bad = bad || F::bad(acc);
                 }
+                if (F::kChecked && __builtin_expect(bad, 0)) {
+#pragma unroll
+                    for (int e = 0; e < W; e++) {
+                        T acc = in[q].e[e];
+#pragma unroll
+                        for (int k = 0; k < P; k++)
+                            if (k != q) acc = Elem<T, OP>::f(acc, in[k].e[e]);
+                        out.e[e] = acc;
+                    }
+                }
+                __builtin_nontemporal_store(out.v, dst + base + u * 64 + lane);
             }
-            __builtin_nontemporal_store(out.v, dst + u * 64 + lane);
+        });
+    };
+    if constexpr (!PERSIST) {
+        load(blockIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; u++) tile[0][w][u * 64 + lane] = v[u];
+        __syncthreads();
+        fold_store(0, blockIdx.x);
+    } else {
+        const size_t ntiles = (nvec + V - 1) / V;
+        size_t t = blockIdx.x;
+        if (t < ntiles) load(t);
+        for (int b = 0; t < ntiles; t += gridDim.x, b ^= 1) {
+#pragma unroll
+            for (int u = 0; u < U; u++) tile[b][w][u * 64 + lane] = v[u];
+            __syncthreads();
+            if (t + gridDim.x < ntiles) load(t + gridDim.x);
+            fold_store(b, t);
         }
-    });
+    }
 }
 
 template <typename T, int OP, int P, bool ORDERED>
@@ -403,24 +448,41 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
-    constexpr int U = TeamShape<T, OP, P>::U;
     size_t head = phase ? (16 - phase) / sizeof(T) : 0;
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;
     const size_t tail_start = head + nvec * W;
     const int nedge = (int) (head + (n - tail_start));
     if constexpr (TeamShape<T, OP, P>::kLds) {
-        constexpr int UL = OSGPU_TEAM_LDS_U;
+        constexpr int UL = TeamShape<T, OP, P>::kLdsU;
+        constexpr bool PERSIST = OSGPU_TEAM_LDS_PERSIST != 0;
         size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
         if (blocks == 0) blocks = 1;
-        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
-                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge);
-        return hipGetLastError();
+        if (PERSIST) {  // the workgroups that fit on the device at once
+            static const size_t resident = [] {
+                int dev = 0, cus = 0, per = 0;
+                (void) hipGetDevice(&dev);
+                if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                        hipSuccess ||
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per, team_lds_kernel<T, OP, P, ORDERED, UL, PERSIST>, 64 * P, 0) !=
+                        hipSuccess)
+                    cus = per = 0;
+                (void) hipGetLastError();
+                return (size_t) std::max(cus, 1) * (size_t) std::max(per, 1);
+            }();
+            blocks = std::min(blocks, resident);
+        }
+        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL, PERSIST>),
+                           dim3((unsigned) blocks), dim3(64 * P), 0, s, a, nvec, head, tail_start,
+                           nedge);
+    } else {  // (not instantiated where the LDS form is used)
+        constexpr int U = TeamShape<T, OP, P>::U;
+        size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);
+        if (blocks == 0) blocks = 1;
+        hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
+                           dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge);
     }
-    size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
-                       dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge);
     return hipGetLastError();
 }
 

@@ -34,9 +34,29 @@ def child(mode):
     L = osgpu.load()
     k = bench.team_kernel_rate(L, torch, n, 20, P=2)
     api = bench.api_call_time(n, reps=reps)
+    # the team kernel alone over the very arrays the call uses (the call's
+    # heap layout: both PEs' slices of one allocation, target at the next
+    # 4 KiB past the source), one launch over both shards, HIP events
+    import ctypes
+    from support import team as T
+    tm = T.Team(2, 2 * n * 8 + 8192, device=True)
+    toff = (n * 8 + 4095) // 4096 * 4096
+    for pe in range(2):
+        tm.buf[pe * tm.H: pe * tm.H + n * 8].view(torch.float64).uniform_(1, 2)
+    S = (ctypes.c_void_p * 2)(tm.ptr(0, 0), tm.ptr(1, 0))
+    D = (ctypes.c_void_p * 2)(tm.ptr(0, toff), tm.ptr(1, toff))
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    torch.cuda.synchronize()
+
+    def launch():
+        assert L.osgpu_team_combine(5, 0, 2, D, S, n, sp) == 0
+    for _ in range(3):
+        launch()
+    k_layout = bench.span_per_launch(torch, st, launch, 20)
     print(json.dumps({"mode": mode, "n": n, "ms_per_call": api["team"]["ms_per_call"],
-                      "kernel_us": k["kernel_avg_us"], "pull_ms_per_call": api["pull"]["ms_per_call"]}),
-          flush=True)
+                      "kernel_us": k["kernel_avg_us"], "kernel_us_call_layout": k_layout * 1e6,
+                      "pull_ms_per_call": api["pull"]["ms_per_call"]}), flush=True)
 
 
 def main():
@@ -67,6 +87,7 @@ def main():
         call_us = rec["ms_per_call"] * 1e3
         rec["frac_call"] = 4 * rec["n"] * 8 / (call_us * 1e-6) / 8e12
         rec["frac_kernel"] = 4 * rec["n"] * 8 / (rec["kernel_us"] * 1e-6) / 8e12
+        rec["frac_kernel_call_layout"] = 4 * rec["n"] * 8 / (rec["kernel_us_call_layout"] * 1e-6) / 8e12
         print(json.dumps(rec), flush=True)
         out.write(json.dumps(rec) + "\n")
         out.flush()

@@ -54,6 +54,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     ldprof) step ldprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ldprof -o run --output-format csv -- python3 tools/ld_rocprof.py run &&
             python3 tools/ld_rocprof.py parse gpurun_out/ldprof gpurun_out/ldprof.log gpurun_out/ld_rocprof.json ;;
     callov) step callov 600 python -u tools/call_overhead.py ;;
+    smallenv) step smallenv 600 python -u tools/small_call_env.py ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;

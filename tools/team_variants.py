@@ -36,7 +36,11 @@ VARIANTS = {
     "pipe_g1": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_G8=1", "-DOSGPU_TEAM_GH=1",
                        "-DOSGPU_TEAM_PEROUT=0"]),
     "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
-    "tree2": (None, []),                              # round 4: per-output folds, integer pipeline
+    "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # round 4 register form (per-output, int pipeline)
+    "final": (None, []),                              # the tree's defaults
+    "persist": (None, ["-DOSGPU_TEAM_LDS_PERSIST=1"]),
+    "persist_u2": (None, ["-DOSGPU_TEAM_LDS_PERSIST=1", "-DOSGPU_TEAM_LDS_U=2",
+                          "-DOSGPU_TEAM_LDS_U8=2"]),
     "lds5": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5"]),
     "lds2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=2"]),
     "lds5u2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5", "-DOSGPU_TEAM_LDS_U=2"]),
