@@ -100,13 +100,9 @@ __device__ __forceinline__ void store_out(u32x4 *p, u32x4 v)
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-// one lane: wait until f[0..P) >= epoch; false (and the error word set) on
-// timeout.  acquire: the caller reads what the members wrote before their
-// flags (the entry barrier: their sources; the staged exit: my result
-// slot); the device form's exit wait only signals the host, which reads
-// nothing through this GPU's caches
+// one lane: wait until f[0..P) >= epoch; false (and the error word set) on timeout
 __device__ bool wait_epoch(const unsigned long long *f, int P, unsigned long long epoch,
-                           unsigned long long timeout, int *err, int code, bool acquire = true)
+                           unsigned long long timeout, int *err, int code)
 {
     const unsigned long long t0 = (unsigned long long) wall_clock64();
     for (int j = 0; j < P; j++) {
@@ -118,18 +114,14 @@ __device__ bool wait_epoch(const unsigned long long *f, int P, unsigned long lon
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    if (acquire) __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     return true;
 }
 
-// The host-mapped completion word of a device-form call.  Relaxed: every
-// byte the call wrote was released system-wide before its done flags (mine
-// by this grid's fence, the peers' by theirs), and the host reads nothing
-// through this GPU's caches -- a release here would only write back an L2
-// that holds no dirty line of the call.
+// the host-mapped completion word of a device-form call
 __device__ __forceinline__ void signal_host(const FusedArgs &a)
 {
-    __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done_host, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Gate words (my flag area): the key names this call and this launch, so a
@@ -267,7 +259,7 @@ __device__ __forceinline__ void fused_done(const FusedArgs &a)
 {
     if (a.resume == 2) {
         if (blockIdx.x == 0 && threadIdx.x == 0 &&
-            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2, false))
+            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
             signal_host(a);
         return;
     }
@@ -275,7 +267,7 @@ __device__ __forceinline__ void fused_done(const FusedArgs &a)
     __syncthreads();
     if (threadIdx.x == 0 && last_workgroup(a, kFlagTicket)) {
         for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
-        if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2, false))
+        if (wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
             signal_host(a);
     }
 }
@@ -496,8 +488,7 @@ __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
             if (last) {
                 if (a.trace) a.trace[4] = a.trace[5] = (unsigned long long) wall_clock64();
                 for (int i = 0; i < a.P; i++) st_sys(a.flags[i] + kFlagDone + a.me, a.epoch);
-                const bool all = wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2,
-                                            a.host_out != nullptr);
+                const bool all = wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2);
                 if (!a.host_out) {
                     if (all) {
                         if (a.trace) a.trace[6] = (unsigned long long) wall_clock64();
@@ -514,7 +505,7 @@ __global__ __launch_bounds__(kFBlock) void fused_kernel(FusedArgs a)
     } else if (!a.host_out) {
         // continuation at the exit barrier, device form: the done wait only
         if (blockIdx.x == 0 && threadIdx.x == 0 &&
-            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2, false))
+            wait_epoch(a.mine + kFlagDone, a.P, a.epoch, a.timeout, a.err, 2))
             signal_host(a);
         return;
     } else if (blockIdx.x == 0 && threadIdx.x == 0) {

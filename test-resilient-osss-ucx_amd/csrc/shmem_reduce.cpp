@@ -30,10 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
-#include <map>
-#include <mutex>
 #include <thread>
-#include <tuple>
 #include <vector>
 
 #include "../../include/osgpu_reduce.h"
@@ -113,82 +110,30 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
     return idx;
 }
 
-// Members of one active set that are threads of THIS process on the same
-// GPU: after the entry barrier every one of them has registered its call
-// here, and the lowest index of each run of consecutive local members
-// launches the team kernel over the whole run's shards -- one launch of
-// the full grid per GPU instead of one per PE thread competing for the same
-// CUs (the second barrier then waited ~15 us for the later of the
-// concurrent half-grids, profiles/r04_call_overhead_1.jsonl).  Calls on a
-// set are matched by a per-thread sequence number: OpenSHMEM members call
-// a set's collectives in the same order.  OSGPU_TEAM_LOCAL_MERGE=0: off.
-struct LocalCall {
-    unsigned mask = 0;  // active-set indices of the local members
-    int left = 0;       // registered members not yet done
-};
-std::mutex g_local_mu;
-std::map<std::tuple<int, int, int, int, unsigned long long>, LocalCall> g_local;
-thread_local std::map<std::tuple<int, int, int, int>, unsigned long long> t_local_seq;
-
-bool local_merge()
-{
-    static const bool on = [] {
-        const char *e = getenv("OSGPU_TEAM_LOCAL_MERGE");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return on;
-}
-
 void run_team(const Call &c, const std::vector<const void *> &srcs,
               const std::vector<void *> &dsts, int idx)
 {
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
-    const int es = (int) (s > 16 ? 16 : s);
-    const bool merge = local_merge() && c.PE_size <= 32;
-    int dev = 0;
-    HIPCHK(c.name, hipGetDevice(&dev));
-    const auto set = std::make_tuple(c.PE_start, c.step, c.PE_size, dev);
-    std::tuple<int, int, int, int, unsigned long long> key;
-    if (merge) {
-        key = std::tuple_cat(set, std::make_tuple(++t_local_seq[set]));
-        std::lock_guard<std::mutex> lk(g_local_mu);
-        LocalCall &L = g_local[key];
-        L.mask |= 1u << idx;
-        L.left++;
-    }
-    t_last_path = OSGPU_RAN_TEAM;
-    call_trace(c.me, 0, "start");
-    entry_sync(c.name, st);
-    call_trace(c.me, 1, "entry_sync");
-    barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
-    call_trace(c.me, 2, "barrier1");
-    // my launch: my own shard, or (merged) the shards of the run of local
-    // members I lead; none when a lower local neighbour leads my run
-    int first = idx, last = idx;
-    if (merge) {
-        unsigned mask;
-        {
-            std::lock_guard<std::mutex> lk(g_local_mu);
-            mask = g_local[key].mask;
-        }
-        if (idx > 0 && (mask >> (idx - 1) & 1u)) first = last = -1;  // led by a neighbour
-        else
-            while (last + 1 < c.PE_size && (mask >> (last + 1) & 1u)) last++;
-    }
-    long long lo = 0, hi = 0, t = 0;
-    if (first >= 0) {
-        osgpu_shard_range(c.nreduce, c.PE_size, first, es, &lo, &t);
-        osgpu_shard_range(c.nreduce, c.PE_size, last, es, &t, &hi);
-    }
+    long long lo = 0, hi = 0;
+    osgpu_shard_range(c.nreduce, c.PE_size, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
     std::vector<const void *> sp(c.PE_size);
     std::vector<void *> dp(c.PE_size);
     for (int i = 0; i < c.PE_size; i++) {
         sp[i] = (const char *) srcs[i] + (size_t) lo * s;
         dp[i] = (char *) dsts[i] + (size_t) lo * s;
     }
-    DBG("%s PE %d: team path, members %d..%d: [%lld, %lld) of %d, P=%d", c.name, c.me, first,
-        last, lo, hi, c.nreduce, c.PE_size);
+    t_last_path = OSGPU_RAN_TEAM;
+    DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
+        c.nreduce, c.PE_size);
+    // (PE threads of one process sharing a GPU could launch one full grid
+    // for all their shards instead of one per thread: measured no faster,
+    // profiles/r04_call_overhead_3.jsonl / _4.jsonl, and not kept)
+    call_trace(c.me, 0, "start");
+    entry_sync(c.name, st);
+    call_trace(c.me, 1, "entry_sync");
+    barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
+    call_trace(c.me, 2, "barrier1");
     if (hi > lo) {
         hipError_t e = osgpu::launch_team(c.type, c.op, c.PE_size, dp.data(), sp.data(),
                                           (size_t) (hi - lo), st);
@@ -202,11 +147,6 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     barrier(c);  // src/reductions.c:113 -- every shard of my target is written
     call_trace(c.me, 5, "barrier2");
     call_trace(c.me, 6, "end");
-    if (merge) {
-        std::lock_guard<std::mutex> lk(g_local_mu);
-        auto it = g_local.find(key);
-        if (it != g_local.end() && --it->second.left == 0) g_local.erase(it);
-    }
 }
 
 // Push form of the team exchange (osgpu_set_team_exchange(1)): every byte

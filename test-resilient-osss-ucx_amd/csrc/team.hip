@@ -16,7 +16,6 @@
 #include <stdint.h>
 #include <stddef.h>
 
-#include <algorithm>
 #include <type_traits>
 
 #include "combine.hpp"
@@ -92,12 +91,7 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_LDS_U8
 #define OSGPU_TEAM_LDS_U8 4
 #endif
-// 1: the LDS form as a persistent grid (workgroups resident at once per
-// CU x CUs) walking tiles, two LDS tile buffers: a wave's loads of its next
-// tile are in flight while it folds and stores this one
-#ifndef OSGPU_TEAM_LDS_PERSIST
-#define OSGPU_TEAM_LDS_PERSIST 0
-#endif
+
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
 // the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
 // (same interleaved A/B)
@@ -315,21 +309,18 @@ __device__ __forceinline__ X pick(const X (&x)[P], int k)
 // stream per wave, as the copy kernel); after the barrier wave q folds the
 // tile of all P inputs from LDS in member q's order and streams member q's
 // target tile (one write stream per wave).  HBM bytes as the register form
-// (2*P*s per element); the LDS carries P reads of every staged byte.
-// PERSIST: the grid walks the tiles (tile t, t + gridDim.x, ...) with two
-// LDS buffers; a wave's loads of its next tile are issued right after the
-// barrier, so they are in flight while it folds and stores this one (the
-// barrier of the next tile orders every wave's reads of a buffer before
-// anyone overwrites it two tiles later).
-template <typename T, int OP, int P, bool ORDERED, int U, bool PERSIST>
+// (2*P*s per element); the LDS carries P reads of every staged byte.  (A
+// persistent grid walking the tiles with two LDS buffers, the next tile's
+// loads in flight during this one's folds, ran 2-17 % slower at 3-8
+// members: profiles/r04_team_sweep_4.jsonl.)
+template <typename T, int OP, int P, bool ORDERED, int U>
 __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                           size_t head, size_t tail_start,
                                                           int nedge)
 {
     constexpr int W = 16 / sizeof(T);
     constexpr int V = 64 * U;  // vectors per member per tile
-    constexpr int NB = PERSIST ? 2 : 1;
-    __shared__ u32x4 tile[NB][P][V];
+    __shared__ u32x4 tile[P][V];
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -355,7 +346,7 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
     using F = Fast<T, OP>;
     // member q's fold of element e: x[q] first, then the others ascending
     // (order-independent integer ops: ascending for every q)
-    auto fold_store = [&](int b, size_t t) {
+    auto fold_store = [&](size_t t) {
         const size_t base = t * V;
         const bool whole = base + V <= nvec;
         Rounds<0, P>::run([&](auto qc) {
@@ -366,7 +357,7 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
                 if (!whole && base + u * 64 + lane >= nvec) continue;
                 TVec<T> in[P], out;
 #pragma unroll
-                for (int p = 0; p < P; p++) in[p].v = tile[b][p][u * 64 + lane];
+                for (int p = 0; p < P; p++) in[p].v = tile[p][u * 64 + lane];
                 bool bad = false;
 #pragma unroll
                 for (int e = 0; e < W; e++) {
@@ -391,24 +382,11 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
             }
         });
     };
-    if constexpr (!PERSIST) {
-        load(blockIdx.x);
+    load(blockIdx.x);
 #pragma unroll
-        for (int u = 0; u < U; u++) tile[0][w][u * 64 + lane] = v[u];
-        __syncthreads();
-        fold_store(0, blockIdx.x);
-    } else {
-        const size_t ntiles = (nvec + V - 1) / V;
-        size_t t = blockIdx.x;
-        if (t < ntiles) load(t);
-        for (int b = 0; t < ntiles; t += gridDim.x, b ^= 1) {
-#pragma unroll
-            for (int u = 0; u < U; u++) tile[b][w][u * 64 + lane] = v[u];
-            __syncthreads();
-            if (t + gridDim.x < ntiles) load(t + gridDim.x);
-            fold_store(b, t);
-        }
-    }
+    for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
+    __syncthreads();
+    fold_store(blockIdx.x);
 }
 
 template <typename T, int OP, int P, bool ORDERED>
@@ -455,27 +433,10 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
     const int nedge = (int) (head + (n - tail_start));
     if constexpr (TeamShape<T, OP, P>::kLds) {
         constexpr int UL = TeamShape<T, OP, P>::kLdsU;
-        constexpr bool PERSIST = OSGPU_TEAM_LDS_PERSIST != 0;
         size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
         if (blocks == 0) blocks = 1;
-        if (PERSIST) {  // the workgroups that fit on the device at once
-            static const size_t resident = [] {
-                int dev = 0, cus = 0, per = 0;
-                (void) hipGetDevice(&dev);
-                if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                        hipSuccess ||
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &per, team_lds_kernel<T, OP, P, ORDERED, UL, PERSIST>, 64 * P, 0) !=
-                        hipSuccess)
-                    cus = per = 0;
-                (void) hipGetLastError();
-                return (size_t) std::max(cus, 1) * (size_t) std::max(per, 1);
-            }();
-            blocks = std::min(blocks, resident);
-        }
-        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL, PERSIST>),
-                           dim3((unsigned) blocks), dim3(64 * P), 0, s, a, nvec, head, tail_start,
-                           nedge);
+        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
+                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge);
     } else {  // (not instantiated where the LDS form is used)
         constexpr int U = TeamShape<T, OP, P>::U;
         size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);

@@ -2,9 +2,9 @@
 """call_overhead.py -- where the whole-call time of the TEAM path goes
 (bench.py roofline_call: shmem_double_sum_to_all, 2 PEs as pthreads on one
 GPU, nreduce = 64 Mi, src/reductions.c:82,113 barriers), per completion-wait
-mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait) and with or
-without the merged launch of co-resident PE threads (shmem_reduce.cpp
-run_team, OSGPU_TEAM_LOCAL_MERGE).  Each mode
+mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait).  (Round-4
+files _1.._4 also compare a merged launch of co-resident PE threads,
+OSGPU_TEAM_LOCAL_MERGE, since removed: it was no faster.)  Each mode
 runs in its own process (the mode is read once) with OSGPU_CALL_TRACE=1:
 PE 0's host clock at entry sync, barrier 1, launch, completion wait,
 barrier 2; the median of every phase over the calls, beside the call time
@@ -62,8 +62,8 @@ def child(mode):
 def main():
     out = open(os.path.join(ROOT, "gpurun_out", "call_overhead.jsonl"), "a")
     # MODE = <OSGPU_SYNC>[+nomerge]: +nomerge sets OSGPU_TEAM_LOCAL_MERGE=0
-    # (one launch per PE thread, as in round 3)
-    for mode in os.environ.get("CO_MODES", "block+nomerge,block,word").split(","):
+    # (meaningful only for the round-4 builds that had the merged launch)
+    for mode in os.environ.get("CO_MODES", "block,word,block,word").split(","):
         sync, _, extra = mode.partition("+")
         env = dict(os.environ, OSGPU_SYNC=sync, OSGPU_CALL_TRACE="1")
         if extra == "nomerge":
