@@ -376,7 +376,7 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     # the form team.hip launches for double sum (TeamShape): the register
     # kernel at 2 members, the LDS-staged one (U = 4) from 3 on
     kern = (f"team_vec_kernel<double, 0, {P}, true>" if P == 2
-            else f"team_lds_kernel<double, 0, {P}, true, 4, false>")
+            else f"team_lds_kernel<double, 0, {P}, true, 4>")
     tr = load_traffic(kern, n)
     frac = B / kavg / 1e9 / HBM_PEAK_GBS
     cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
