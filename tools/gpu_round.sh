@@ -51,6 +51,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     copyvar) step copyvar 600 python -u tools/team_variants.py run_copy ;;
     teamvar) step teamvar 900 python -u tools/team_variants.py run ;;
     sweep) step sweep 900 python -u tools/team_variants.py run_sweep ;;
+    place) step place 600 python -u tools/team_variants.py run_place ;;
     ldprof) step ldprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ldprof -o run --output-format csv -- python3 tools/ld_rocprof.py run &&
             python3 tools/ld_rocprof.py parse gpurun_out/ldprof gpurun_out/ldprof.log gpurun_out/ld_rocprof.json ;;
     callov) step callov 600 python -u tools/call_overhead.py ;;

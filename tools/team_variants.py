@@ -38,9 +38,8 @@ VARIANTS = {
     "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
     "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # round 4 register form (per-output, int pipeline)
     "final": (None, []),                              # the tree's defaults
-    "persist": (None, ["-DOSGPU_TEAM_LDS_PERSIST=1"]),
-    "persist_u2": (None, ["-DOSGPU_TEAM_LDS_PERSIST=1", "-DOSGPU_TEAM_LDS_U=2",
-                          "-DOSGPU_TEAM_LDS_U8=2"]),
+    # (round 4 also measured a persistent LDS form, OSGPU_TEAM_LDS_PERSIST,
+    # since removed: profiles/r04_team_sweep_4.jsonl)
     "lds5": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5"]),
     "lds2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=2"]),
     "lds5u2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5", "-DOSGPU_TEAM_LDS_U=2"]),
@@ -282,6 +281,74 @@ def run_sweep():
                 outf.flush()
 
 
+def run_place():
+    """The team kernel's form against placement: double sum at P in TV_PS
+    (default 4, 8), TV_TRIALS fresh allocations (2P arrays of n = 64 Mi
+    doubles, as bench.py's roofline_team_by_members), every variant in
+    TV_NAMES and the same-mix copy interleaved on each allocation, TV_ROUNDS
+    event spans of REPS launches each.  One JSON line per (P, trial,
+    variant); gpurun_out/team_place.jsonl."""
+    import ctypes
+    import torch
+    torch.cuda.init()
+    names = os.environ.get("TV_NAMES", "final,tree2").split(",")
+    libs = {}
+    for name in names:
+        L = ctypes.CDLL(os.path.join(VARLIB, name, "libosgpu_reduce.so"), mode=os.RTLD_LOCAL)
+        L.osgpu_team_combine.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.osgpu_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_void_p]
+        libs[name] = L
+    C = libs[names[0]]
+    reps = int(os.environ.get("REPS", "5"))
+    rounds = int(os.environ.get("TV_ROUNDS", "5"))
+    trials = int(os.environ.get("TV_TRIALS", "5"))
+    n = int(os.environ.get("TV_N", str(64 << 20)))
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    outf = open(os.path.join(ROOT, "gpurun_out", "team_place.jsonl"), "a")
+    for P in [int(p) for p in os.environ.get("TV_PS", "4,8").split(",")]:
+        for trial in range(trials):
+            g = torch.Generator(device="cuda").manual_seed(100 * P + trial)
+            srcs = [torch.empty(n, dtype=torch.float64, device="cuda").uniform_(1, 2, generator=g)
+                    for _ in range(P)]
+            dsts = [torch.empty(n, dtype=torch.float64, device="cuda") for _ in range(P)]
+            S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs])
+            D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts])
+            N = (ctypes.c_size_t * P)(*([n * 8] * P))
+            torch.cuda.synchronize()
+            for name in names:
+                assert libs[name].osgpu_team_combine(5, 0, P, D, S, n, sp) == 0
+            assert C.osgpu_copy(D, S, N, P, sp) == 0
+            st.synchronize()
+            times = {name: [] for name in names + ["copy"]}
+            for _ in range(rounds):
+                for name in names + ["copy"]:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(reps):
+                        if name == "copy":
+                            C.osgpu_copy(D, S, N, P, sp)
+                        else:
+                            libs[name].osgpu_team_combine(5, 0, P, D, S, n, sp)
+                    e1.record(st)
+                    e1.synchronize()
+                    times[name].append(e0.elapsed_time(e1) * 1e3 / reps)
+            B = 2 * P * n * 8
+            cus = sorted(times["copy"])[rounds // 2]
+            for name in names:
+                us = sorted(times[name])[rounds // 2]
+                rec = {"P": P, "trial": trial, "variant": name, "us": us, "frac": B / us / 8e6,
+                       "copy_frac": B / cus / 8e6, "frac_of_copy": cus / us}
+                print(json.dumps(rec), flush=True)
+                outf.write(json.dumps(rec) + "\n")
+            outf.flush()
+            del srcs, dsts
+            torch.cuda.empty_cache()
+
+
 def build_copy():
     subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
     others = ["combine.o", "team.o", "fused.o", "verify.o", "longdouble.o", "runtime.o", "heap.o",
@@ -354,5 +421,6 @@ def run_copy():
 
 
 if __name__ == "__main__":
-    {"build": build, "run": run, "run_sweep": run_sweep, "build_copy": build_copy,
+    {"build": build, "run": run, "run_sweep": run_sweep, "run_place": run_place,
+     "build_copy": build_copy,
      "run_copy": run_copy}[sys.argv[1]]()
