@@ -376,13 +376,14 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     # the form team.hip launches for double sum (TeamShape): the register
     # kernel at 2 members, the LDS-staged one (U = 4) from 3 on
     kern = (f"team_vec_kernel<double, 0, {P}, true>" if P == 2
-            else f"team_lds_kernel<double, 0, {P}, true, 4>")
+            else f"team_lds_kernel<double, 0, {P}, true, 4")   # (PMC files' key)
     tr = load_traffic(kern, n)
     frac = B / kavg / 1e9 / HBM_PEAK_GBS
     cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": frac, "traffic": tr.get("bytes_per_launch") if tr else None,
-           "kernel": "osgpu::" + kern.replace("<double, 0,", "<double, SUM,"),
+           "kernel": ("osgpu::" + kern.replace("<double, 0,", "<double, SUM,") +
+                      ("" if P == 2 else ">")),
            "members": P, "nreduce": n,
            "kernel_avg_us": kavg * 1e6,
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",

@@ -81,7 +81,11 @@ constexpr int kTeamBlock = 256;
 // 0.44-0.62 (profiles/r04_team_sweep_2.jsonl).  On another box U = 4 beat
 // U = 2 at 3-8 members (1.01-1.02 against 0.95-0.97 of the copy at 5-7,
 // r04_team_sweep_3.jsonl); the complex double product at 8 members stays
-// on the register form there (0.90 against 0.76-0.89 staged)
+// on the register form there (0.90 against 0.76-0.89 staged).  With the
+// measurement order rotated per round (a fixed order biased identical
+// kernels by up to 4 %), the LDS form leads the register form at every
+// member count from 3 to 8 on five fresh allocations per count
+// (r04_team_place_3.jsonl: 8 members 0.949 against 0.920 of the copy)
 #ifndef OSGPU_TEAM_LDS_MIN_P
 #define OSGPU_TEAM_LDS_MIN_P 3
 #endif
@@ -312,7 +316,8 @@ __device__ __forceinline__ X pick(const X (&x)[P], int k)
 // (2*P*s per element); the LDS carries P reads of every staged byte.  (A
 // persistent grid walking the tiles with two LDS buffers, the next tile's
 // loads in flight during this one's folds, ran 2-17 % slower at 3-8
-// members: profiles/r04_team_sweep_4.jsonl.)
+// members: profiles/r04_team_sweep_4.jsonl; two or four members per wave,
+// fewer waves per workgroup, no faster: r04_team_place_3.jsonl.)
 template <typename T, int OP, int P, bool ORDERED, int U>
 __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                           size_t head, size_t tail_start,

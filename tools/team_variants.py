@@ -38,6 +38,8 @@ VARIANTS = {
     "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
     "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # round 4 register form (per-output, int pipeline)
     "final": (None, []),                              # the tree's defaults
+    # (round 4 also measured 2 / 4 members per wave in the LDS form,
+    # OSGPU_TEAM_LDS_K, since removed: profiles/r04_team_place_2/3.jsonl)
     # (round 4 also measured a persistent LDS form, OSGPU_TEAM_LDS_PERSIST,
     # since removed: profiles/r04_team_sweep_4.jsonl)
     "lds5": (None, ["-DOSGPU_TEAM_LDS_MIN_P=5"]),
@@ -58,7 +60,8 @@ OTHERS = ["fused.o", "verify.o", "longdouble.o", "copy.o", "runtime.o", "heap.o"
 
 
 def build():
-    subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
+    if not os.environ.get("TV_NO_MAKE"):   # (TV_NO_MAKE: the tree's objects as they are)
+        subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
     procs = []
     for name, (rev, flags) in VARIANTS.items():
         d = os.path.join(VAR, name)
@@ -254,8 +257,11 @@ def run_sweep():
                 for _ in range(2):
                     assert C.osgpu_copy(D1, S, N, P, sp) == 0
                 times = {name: [] for name in names + ["copy"]}
-                for _ in range(rounds):
-                    for name in names + ["copy"]:
+                order = names + ["copy"]
+                for rnd in range(rounds):
+                    # rotated each round: a fixed order biased identical
+                    # kernels by up to 4 % by position (r04_team_place_2)
+                    for name in order[rnd % len(order):] + order[:rnd % len(order)]:
                         e0 = torch.cuda.Event(enable_timing=True)
                         e1 = torch.cuda.Event(enable_timing=True)
                         e0.record(st)
@@ -323,8 +329,9 @@ def run_place():
             assert C.osgpu_copy(D, S, N, P, sp) == 0
             st.synchronize()
             times = {name: [] for name in names + ["copy"]}
-            for _ in range(rounds):
-                for name in names + ["copy"]:
+            order = names + ["copy"]
+            for rnd in range(rounds):
+                for name in order[rnd % len(order):] + order[:rnd % len(order)]:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(st)
