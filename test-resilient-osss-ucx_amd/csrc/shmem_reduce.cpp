@@ -127,8 +127,9 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
         c.nreduce, c.PE_size);
     // (PE threads of one process sharing a GPU could launch one full grid
-    // for all their shards instead of one per thread: measured no faster,
-    // profiles/r04_call_overhead_3.jsonl / _4.jsonl, and not kept)
+    // for all their shards instead of one per thread, or queue their
+    // shards on one stream: both measured slower than these concurrent
+    // half-grids, profiles/r04_call_overhead_3.jsonl .. _5.jsonl, not kept)
     call_trace(c.me, 0, "start");
     entry_sync(c.name, st);
     call_trace(c.me, 1, "entry_sync");

@@ -68,6 +68,8 @@ def main():
         env = dict(os.environ, OSGPU_SYNC=sync, OSGPU_CALL_TRACE="1")
         if extra == "nomerge":
             env["OSGPU_TEAM_LOCAL_MERGE"] = "0"
+        if extra == "shared":   # (r04_call_overhead_5: one team stream per
+            env["OSGPU_TEAM_STREAM"] = "shared"    # device, since removed)
         r = subprocess.run([sys.executable, __file__, "child", mode], env=env, capture_output=True,
                            text=True, timeout=600)
         if r.returncode != 0:
