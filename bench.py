@@ -317,8 +317,8 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
 
 def team_kernel_rate(L, torch, n, reps, P=2):
     """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
-    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,2>
-    / team_lds_kernel<double,SUM,P> from 3 members
+    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>,
+    team_lds_kernel<double,SUM,P> at 3 and 4 members
     through the C ABI (osgpu_team_combine), one launch over all n elements --
     the work the P PEs' shard launches of a P-PE call do together: reads
     every source once, writes every target (PE q: x_q + the others in
@@ -373,17 +373,18 @@ def team_kernel_rate(L, torch, n, reps, P=2):
         copy()
     cavg = span_per_launch(torch, st, copy, reps)
     B = 2 * P * n * 8
-    # the form team.hip launches for double sum (TeamShape): the register
-    # kernel at 2 members, the LDS-staged one (U = 4) from 3 on
-    kern = (f"team_vec_kernel<double, 0, {P}, true>" if P == 2
-            else f"team_lds_kernel<double, 0, {P}, true, 4")   # (PMC files' key)
+    # the form team.hip launches for double sum (TeamShape): the LDS-staged
+    # kernel (U = 4) at 3 and 4 members, the register kernel otherwise
+    lds = 3 <= P <= 4
+    kern = (f"team_lds_kernel<double, 0, {P}, true, 4" if lds    # (PMC files' key)
+            else f"team_vec_kernel<double, 0, {P}, true>")
     tr = load_traffic(kern, n)
     frac = B / kavg / 1e9 / HBM_PEAK_GBS
     cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": frac, "traffic": tr.get("bytes_per_launch") if tr else None,
            "kernel": ("osgpu::" + kern.replace("<double, 0,", "<double, SUM,") +
-                      ("" if P == 2 else ">")),
+                      (">" if lds else "")),
            "members": P, "nreduce": n,
            "kernel_avg_us": kavg * 1e6,
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
@@ -1256,8 +1257,8 @@ def bench_multi(args):
         res["roofline"] = {
             "bound": "xgmi", "achieved": per_dir, "peak": peak, "unit": "GB/s",
             "frac": per_dir / peak, "traffic": None,
-            "kernel": (f"osgpu::team_vec_kernel<double, SUM, {world}>" if world == 2
-                       else f"osgpu::team_lds_kernel<double, SUM, {world}>"),
+            "kernel": (f"osgpu::team_lds_kernel<double, SUM, {world}>" if 3 <= world <= 4
+                       else f"osgpu::team_vec_kernel<double, SUM, {world}>"),
             "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
                      f"second: the shard reads from every peer plus every peer's writes of its "
                      f"shard into this GPU's target (it sends as many); peak = {world - 1} x "

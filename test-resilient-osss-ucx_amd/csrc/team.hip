@@ -73,21 +73,23 @@ constexpr int kTeamBlock = 256;
 #define OSGPU_TEAM_PEROUT 1
 #endif
 // from this many members on: the LDS-staged kernel (team_lds_kernel), one
-// wave per member, 16-B vectors per lane per tile OSGPU_TEAM_LDS_U (below 8
-// members) and OSGPU_TEAM_LDS_U8 (8).  On a box whose copy kernel moved
-// 0.76 of 8 TB/s at 8 ranges it reached 0.938 of that copy against 0.898
-// for the register form at 8 members, 0.96-1.04 against 0.91-0.95 at 5-7;
-// 8 vectors per lane (64 KiB of LDS per workgroup at 8 members) fell to
-// 0.44-0.62 (profiles/r04_team_sweep_2.jsonl).  On another box U = 4 beat
-// U = 2 at 3-8 members (1.01-1.02 against 0.95-0.97 of the copy at 5-7,
-// r04_team_sweep_3.jsonl); the complex double product at 8 members stays
-// on the register form there (0.90 against 0.76-0.89 staged).  With the
-// measurement order rotated per round (a fixed order biased identical
-// kernels by up to 4 %), the LDS form leads the register form at every
-// member count from 3 to 8 on five fresh allocations per count
-// (r04_team_place_3.jsonl: 8 members 0.949 against 0.920 of the copy)
+// wave per member, OSGPU_TEAM_LDS_U 16-B vectors per lane per tile (U = 4:
+// 1.01-1.02 of the copy against 0.95-0.97 for U = 2 at 3-7 members,
+// profiles/r04_team_sweep_3.jsonl; U = 8, 64 KiB of LDS per workgroup at 8
+// members, 0.44-0.62, r04_team_sweep_2.jsonl)
 #ifndef OSGPU_TEAM_LDS_MIN_P
 #define OSGPU_TEAM_LDS_MIN_P 3
+#endif
+// ... up to this many members; above, the register form.  On boxes whose
+// P-range copy itself is fast (0.81-0.84 of 8 TB/s) the register form led
+// at 5-8 members by 5-7 % (0.956 against 0.884 of the copy at 8, five
+// allocations, order rotated, r04_team_place_4.jsonl), on slow ones (0.75-
+// 0.77) the LDS form by 3-5 % (r04_team_place_3.jsonl): in absolute terms
+// the register form's best (0.81 of 8 TB/s at 8 members) is above the LDS
+// form's (0.75), so it keeps 5-8; at 3-4 members the LDS form is ahead or
+// equal on both kinds of box
+#ifndef OSGPU_TEAM_LDS_MAX_P
+#define OSGPU_TEAM_LDS_MAX_P 4
 #endif
 #ifndef OSGPU_TEAM_LDS_U
 #define OSGPU_TEAM_LDS_U 4
@@ -95,6 +97,7 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_LDS_U8
 #define OSGPU_TEAM_LDS_U8 4
 #endif
+
 
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
 // the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
@@ -117,7 +120,7 @@ struct TeamShape {
     // ordered folds above 4 members: fold, check and store one output at a
     // time instead of all P outputs, then all P stores
     static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
-    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P &&
+    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P && P <= OSGPU_TEAM_LDS_MAX_P &&
                                  !(std::is_same<T, cdouble>::value && OP == OP_PROD && P >= 8);
     static constexpr int kLdsU = P >= 8 ? OSGPU_TEAM_LDS_U8 : OSGPU_TEAM_LDS_U;
     // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
@@ -351,14 +354,15 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
     using F = Fast<T, OP>;
     // member q's fold of element e: x[q] first, then the others ascending
     // (order-independent integer ops: ascending for every q)
-    auto fold_store = [&](size_t t) {
+    // the vectors [u0, u1) of the tile
+    auto fold_store = [&](size_t t, int u0, int u1) {
         const size_t base = t * V;
         const bool whole = base + V <= nvec;
         Rounds<0, P>::run([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             if (w != q) return;
 #pragma unroll
-            for (int u = 0; u < U; u++) {
+            for (int u = u0; u < u1; u++) {
                 if (!whole && base + u * 64 + lane >= nvec) continue;
                 TVec<T> in[P], out;
 #pragma unroll
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
 #pragma unroll
     for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
     __syncthreads();
-    fold_store(blockIdx.x);
+    fold_store(blockIdx.x, 0, U);
 }
 
 template <typename T, int OP, int P, bool ORDERED>

@@ -67,7 +67,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic.json &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team.json "team_vec_kernel<double, 0, 2, true>" 32 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team4.json "team_lds_kernel<double, 0, 4, true, 4" 64 &&
-           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team8.json "team_lds_kernel<double, 0, 8, true, 4" 128 ;;
+           python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team8.json "team_vec_kernel<double, 0, 8, true>" 128 ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $((64<<20)) gpurun_out/traffic.json &&

@@ -36,8 +36,11 @@ VARIANTS = {
     "pipe_g1": (None, ["-DOSGPU_TEAM_PIPE=1", "-DOSGPU_TEAM_G8=1", "-DOSGPU_TEAM_GH=1",
                        "-DOSGPU_TEAM_PEROUT=0"]),
     "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
-    "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # round 4 register form (per-output, int pipeline)
+    "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # register form at every P
     "final": (None, []),                              # the tree's defaults
+    # (a two-half LDS tile, OSGPU_TEAM_LDS_SPLIT, measured equal to one and
+    # was removed: profiles/r04_team_place_4.jsonl)
+    "lds8": (None, ["-DOSGPU_TEAM_LDS_MAX_P=8"]),      # LDS form at 3-8 members
     # (round 4 also measured 2 / 4 members per wave in the LDS form,
     # OSGPU_TEAM_LDS_K, since removed: profiles/r04_team_place_2/3.jsonl)
     # (round 4 also measured a persistent LDS form, OSGPU_TEAM_LDS_PERSIST,
