@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--deadline", type=float, default=420.0,
                     help="N>1: print what was measured and exit after this many seconds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="N=1: take roofline.traffic from profiles/ instead of this run's "
+                         "rocprofv3 --pmc passes")
     ap.add_argument("--no-api", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=64 << 20,
                     help="nreduce of the CPU-baseline sample")
@@ -80,10 +83,17 @@ def parse():
 # N = 1
 # --------------------------------------------------------------------------
 
+LIVE_TRAFFIC = {}  # filled by live_traffic() before the line's rooflines are built
+
+
 def load_traffic(kernel="combine_vec_kernel<double, 0, 2>", n=None):
-    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters
-    (profiles/*traffic*.json, written by tools/pmc_traffic.py), newest round
-    last; None if no file covers that kernel at that nreduce."""
+    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters:
+    this run's own passes (LIVE_TRAFFIC) when they produced the kernel, else
+    the newest profiles/*traffic*.json (tools/pmc_traffic.py) covering that
+    kernel at that nreduce, labelled as looked up; None if neither."""
+    live = LIVE_TRAFFIC.get(kernel)
+    if live is not None and (n is None or live.get("nreduce") == n):
+        return live
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
@@ -93,8 +103,61 @@ def load_traffic(kernel="combine_vec_kernel<double, 0, 2>", n=None):
         except Exception:
             continue
         if d.get("kernel") == kernel and (n is None or d.get("nreduce") == n):
-            best = d
+            best = dict(d, source="looked up: profiles/" + os.path.basename(p))
     return best
+
+
+def live_traffic(n, members=(2, 4, 8), reps=5, timeout=120):
+    """HBM bytes per launch measured in THIS run: two child processes,
+    `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes),
+    over tools/pmc_probe.py -- the combine kernel and the team kernel for
+    each member count, on this line's shapes, through the C ABI.  Returns
+    {kernel key: tools/pmc_traffic.traffic() dict} plus "_error" on failure;
+    each pass runs in its own process group, killed at `timeout`."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return {"_error": "rocprofv3 not on PATH"}
+    keys = {"combine_vec_kernel<double, 0, 2>": 24}
+    for P in members:
+        keys[(f"team_lds_kernel<double, 0, {P}, true, 4" if 3 <= P <= 4
+              else f"team_vec_kernel<double, 0, {P}, true>")] = 16 * P
+    tmp = tempfile.mkdtemp(prefix="osgpu_pmc_")
+    dirs = {}
+    t0 = time.time()
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv",
+                   "--", sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"),
+                   str(n), str(reps)] + [str(P) for P in members]
+            p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                 start_new_session=True, cwd=ROOT)
+            try:
+                out, _ = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.communicate()
+                return {"_error": f"{counter} pass killed after {timeout} s"}
+            if p.returncode != 0:
+                tail = out.decode(errors="replace").strip().splitlines()[-3:]
+                return {"_error": f"{counter} pass exit {p.returncode}: {' | '.join(tail)}"}
+            dirs[counter] = d
+        res = {}
+        for k, per_elem in keys.items():
+            r = pmc_traffic.traffic(dirs["FETCH_SIZE"], dirs["WRITE_SIZE"], n, k, per_elem)
+            if r is not None:
+                r["source"] = "live: this run's rocprofv3 passes over tools/pmc_probe.py"
+                res[k] = r
+        res["_seconds"] = time.time() - t0
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def cpu_baseline(n):
@@ -383,6 +446,7 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     cfrac = B / cavg / 1e9 / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": frac, "traffic": tr.get("bytes_per_launch") if tr else None,
+           "traffic_source": tr.get("source") if tr else None,
            "kernel": ("osgpu::" + kern.replace("<double, 0,", "<double, SUM,") +
                       (">" if lds else "")),
            "members": P, "nreduce": n,
@@ -689,11 +753,31 @@ def bench_single(args):
             res.update(extra_kernel_rates(L, torch))
         except Exception as e:  # report, never hide
             res["extra_kernels"] = {"error": repr(e)}
+    # this run's own PMC passes (child processes under rocprofv3); not when
+    # this process is itself being profiled (nested profilers)
+    profiled = any(k.startswith("ROCPROF") for k in os.environ) or \
+        "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if args.no_live_pmc or profiled:
+        res["traffic_live"] = {"skipped": "--no-live-pmc" if args.no_live_pmc
+                               else "this process runs under rocprofv3"}
+    else:
+        try:
+            live = live_traffic(n, (2, 4, 8) if not args.no_extra else ())
+        except Exception as e:  # report, never hide
+            live = {"_error": repr(e)}
+        LIVE_TRAFFIC.update({k: v for k, v in live.items() if not k.startswith("_")})
+        res["traffic_live"] = {
+            "how": "rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, each a child process "
+                   "of this run over tools/pmc_probe.py (the same kernels and shapes through "
+                   "the C ABI, 5 launches each); FETCH_SIZE x2 (gfx950), KiB -> bytes",
+            "kernels": {k: v["traffic_over_algorithmic"] for k, v in LIVE_TRAFFIC.items()},
+            **{k: v for k, v in live.items() if k.startswith("_")}}
     tr = load_traffic(n=n)
     res["roofline"] = {
         "bound": "hbm", "achieved": B / kavg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
         "traffic": tr.get("bytes_per_launch") if tr else None,
+        "traffic_source": tr.get("source") if tr else None,
         "kernel": "osgpu::combine_vec_kernel<double, SUM, 2>",
         "kernel_avg_us": kavg * 1e6,
         "kernel_avg_how": "HIP event span over the K timed launches on the launch stream / K",

@@ -38,6 +38,13 @@ hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *c
                        size_t n, hipStream_t s);
 hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,
                                   size_t n, hipStream_t s);
+// The same over [0, n) split by tiles instead of contiguous shards: of m
+// members sharing one GPU, member k folds the tiles k, k + m, k + 2m, ...
+// (a tile = one workgroup's vectors), so their concurrent grids stream the
+// same address range together (run_team).  m = 1, k = 0: launch_team.
+// hipErrorNotSupported for long double (contiguous shards only).
+hipError_t launch_team_tiles(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                             size_t n, int m, int k, hipStream_t s);
 
 // Byte copy of up to kMaxCopySegs independent ranges in one launch (copy.hip):
 // the data movement of broadcast / collect / fcollect / alltoall.  Sources may

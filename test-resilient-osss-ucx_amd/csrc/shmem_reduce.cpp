@@ -30,7 +30,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/osgpu_reduce.h"
@@ -110,34 +113,85 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
     return idx;
 }
 
+// Members of one active set that are threads of THIS process on the same
+// GPU (threads-as-PEs; mixed topologies): each registers its call here
+// before the entry barrier, so after it every local member is known, and a
+// run of consecutive local members [first, last] folds the union of their
+// shards split by TILES (launch_team_tiles: member k of m takes the tiles k,
+// k + m, ...) instead of one contiguous shard each.  Their grids share the
+// GPU; with contiguous shards the two concurrent half-grids of a 2-PE call
+// streamed two distant ranges and ended ~16 us apart, the whole call taking
+// ~6 % longer than one full grid (profiles/r04_call_overhead_1..4.jsonl).
+// Calls on a set are matched by a per-thread sequence number: OpenSHMEM
+// members call a set's collectives in the same order.
+// OSGPU_TEAM_LOCAL_TILES=0: contiguous shards always.
+struct LocalCall {
+    unsigned mask = 0;  // active-set indices of the local members
+    int left = 0;       // registered members not yet done
+};
+std::mutex g_local_mu;
+std::map<std::tuple<int, int, int, int, unsigned long long>, LocalCall> g_local;
+thread_local std::map<std::tuple<int, int, int, int>, unsigned long long> t_local_seq;
+
+bool local_tiles()
+{
+    static const bool on = [] {
+        const char *e = getenv("OSGPU_TEAM_LOCAL_TILES");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
 void run_team(const Call &c, const std::vector<const void *> &srcs,
               const std::vector<void *> &dsts, int idx)
 {
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
-    long long lo = 0, hi = 0;
-    osgpu_shard_range(c.nreduce, c.PE_size, idx, (int) (s > 16 ? 16 : s), &lo, &hi);
+    const int es = (int) (s > 16 ? 16 : s);
+    const bool tiles = local_tiles() && c.type != osgpu::T_LONGDOUBLE;
+    std::tuple<int, int, int, int, unsigned long long> key;
+    if (tiles) {
+        int dev = 0;
+        HIPCHK(c.name, hipGetDevice(&dev));
+        const auto set = std::make_tuple(c.PE_start, c.step, c.PE_size, dev);
+        key = std::tuple_cat(set, std::make_tuple(++t_local_seq[set]));
+        std::lock_guard<std::mutex> lk(g_local_mu);
+        LocalCall &L = g_local[key];
+        L.mask |= 1u << idx;
+        L.left++;
+    }
+    t_last_path = OSGPU_RAN_TEAM;
+    call_trace(c.me, 0, "start");
+    entry_sync(c.name, st);
+    call_trace(c.me, 1, "entry_sync");
+    barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
+    call_trace(c.me, 2, "barrier1");
+    // the run of consecutive local members I belong to (just me without tiles)
+    int first = idx, last = idx;
+    if (tiles) {
+        unsigned mask;
+        {
+            std::lock_guard<std::mutex> lk(g_local_mu);
+            mask = g_local[key].mask;
+        }
+        while (first > 0 && (mask >> (first - 1) & 1u)) first--;
+        while (last + 1 < c.PE_size && (mask >> (last + 1) & 1u)) last++;
+    }
+    long long lo = 0, hi = 0, t = 0;
+    osgpu_shard_range(c.nreduce, c.PE_size, first, es, &lo, &t);
+    osgpu_shard_range(c.nreduce, c.PE_size, last, es, &t, &hi);
     std::vector<const void *> sp(c.PE_size);
     std::vector<void *> dp(c.PE_size);
     for (int i = 0; i < c.PE_size; i++) {
         sp[i] = (const char *) srcs[i] + (size_t) lo * s;
         dp[i] = (char *) dsts[i] + (size_t) lo * s;
     }
-    t_last_path = OSGPU_RAN_TEAM;
-    DBG("%s PE %d: team path, shard [%lld, %lld) of %d, P=%d", c.name, c.me, lo, hi,
-        c.nreduce, c.PE_size);
-    // (PE threads of one process sharing a GPU could launch one full grid
-    // for all their shards instead of one per thread, or queue their
-    // shards on one stream: both measured slower than these concurrent
-    // half-grids, profiles/r04_call_overhead_3.jsonl .. _5.jsonl, not kept)
-    call_trace(c.me, 0, "start");
-    entry_sync(c.name, st);
-    call_trace(c.me, 1, "entry_sync");
-    barrier(c);  // src/reductions.c:82 -- sources ready, every target writable
-    call_trace(c.me, 2, "barrier1");
+    DBG("%s PE %d: team path, [%lld, %lld) of %d, tiles %d of %d, P=%d", c.name, c.me, lo, hi,
+        c.nreduce, idx - first, last - first + 1, c.PE_size);
     if (hi > lo) {
-        hipError_t e = osgpu::launch_team(c.type, c.op, c.PE_size, dp.data(), sp.data(),
-                                          (size_t) (hi - lo), st);
+        hipError_t e = osgpu::launch_team_tiles(c.type, c.op, c.PE_size, dp.data(), sp.data(),
+                                                (size_t) (hi - lo), last - first + 1,
+                                                idx - first, st);
         if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
     }
     call_trace(c.me, 3, "launch");
@@ -148,6 +202,11 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     barrier(c);  // src/reductions.c:113 -- every shard of my target is written
     call_trace(c.me, 5, "barrier2");
     call_trace(c.me, 6, "end");
+    if (tiles) {
+        std::lock_guard<std::mutex> lk(g_local_mu);
+        auto it = g_local.find(key);
+        if (it != g_local.end() && --it->second.left == 0) g_local.erase(it);
+    }
 }
 
 // Push form of the team exchange (osgpu_set_team_exchange(1)): every byte

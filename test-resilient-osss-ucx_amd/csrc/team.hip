@@ -167,7 +167,7 @@ __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
 template <typename T, int OP, int P, bool ORDERED>
 __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                               size_t head, size_t tail_start,
-                                                              int nedge)
+                                                              int nedge, unsigned tm, unsigned tk)
 {
     constexpr int W = 16 / sizeof(T);
     using S = TeamShape<T, OP, P>;
@@ -181,7 +181,8 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
 #pragma unroll
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
-    const size_t t0 = (size_t) blockIdx.x * (kTeamBlock * U) + threadIdx.x;
+    // tile blockIdx.x * tm + tk (launch_team_tiles; tm = 1, tk = 0: tile blockIdx.x)
+    const size_t t0 = ((size_t) blockIdx.x * tm + tk) * (kTeamBlock * U) + threadIdx.x;
     // fold one vector of every input into one vector of every output: the
     // branch-free fold first, the exact one only for a vector whose results
     // hold a NaN part (rare; elem_ops.hpp Fast) -- no branch per element, so
@@ -324,7 +325,7 @@ __device__ __forceinline__ X pick(const X (&x)[P], int k)
 template <typename T, int OP, int P, bool ORDERED, int U>
 __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                           size_t head, size_t tail_start,
-                                                          int nedge)
+                                                          int nedge, unsigned tm, unsigned tk)
 {
     constexpr int W = 16 / sizeof(T);
     constexpr int V = 64 * U;  // vectors per member per tile
@@ -391,18 +392,22 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
             }
         });
     };
-    load(blockIdx.x);
+    const size_t t = (size_t) blockIdx.x * tm + tk;
+    load(t);
 #pragma unroll
     for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
     __syncthreads();
-    fold_store(blockIdx.x, 0, U);
+    fold_store(t, 0, U);
 }
 
 template <typename T, int OP, int P, bool ORDERED>
-__global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> a, size_t n)
+__global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> a, size_t n,
+                                                                 unsigned tm, unsigned tk)
 {
-    const size_t stride = (size_t) gridDim.x * kTeamBlock;
-    for (size_t i = (size_t) blockIdx.x * kTeamBlock + threadIdx.x; i < n; i += stride) {
+    // tiles of kTeamBlock elements: blockIdx.x * tm + tk, then gridDim.x * tm further
+    const size_t stride = (size_t) gridDim.x * tm * kTeamBlock;
+    for (size_t i = ((size_t) blockIdx.x * tm + tk) * kTeamBlock + threadIdx.x; i < n;
+         i += stride) {
         T x[P], r[P];
 #pragma unroll
         for (int p = 0; p < P; p++) x[p] = a.src[p][i];
@@ -412,9 +417,20 @@ __global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> 
     }
 }
 
+// tiles of m members, this one k-th (launch_team_tiles)
+struct Tiles {
+    unsigned m, k;
+    // of `total` tiles, the ones this member folds (at least one block)
+    size_t blocks(size_t total) const
+    {
+        const size_t b = total > k ? (total - k + m - 1) / m : 0;
+        return b ? b : 1;
+    }
+};
+
 template <typename T, int OP, int P>
 static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size_t n,
-                                hipStream_t s)
+                                Tiles tl, hipStream_t s)
 {
     // integer ops are order-independent (wrapping ring / lattice ops); every
     // floating-point op, min/max included (NaN, signed zero), is not
@@ -428,10 +444,10 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
         same = same && (((uintptr_t) srcs[p] & 15) == phase) && (((uintptr_t) dsts[p] & 15) == phase);
     }
     if (!same) {
-        size_t blocks = (n + kTeamBlock - 1) / kTeamBlock;
-        blocks = blocks > 8192 ? 8192 : (blocks ? blocks : 1);
+        size_t blocks = tl.blocks((n + kTeamBlock - 1) / kTeamBlock);
+        blocks = blocks > 8192 ? 8192 : blocks;
         hipLaunchKernelGGL((team_scalar_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
-                           dim3(kTeamBlock), 0, s, a, n);
+                           dim3(kTeamBlock), 0, s, a, n, tl.m, tl.k);
         return hipGetLastError();
     }
     constexpr int W = 16 / sizeof(T);
@@ -439,45 +455,45 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
     if (head > n) head = n;
     const size_t nvec = (n - head) / W;
     const size_t tail_start = head + nvec * W;
-    const int nedge = (int) (head + (n - tail_start));
+    // the unaligned head and the tail: member 0's first workgroup
+    const int nedge = tl.k == 0 ? (int) (head + (n - tail_start)) : 0;
     if constexpr (TeamShape<T, OP, P>::kLds) {
         constexpr int UL = TeamShape<T, OP, P>::kLdsU;
-        size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
-        if (blocks == 0) blocks = 1;
+        const size_t blocks = tl.blocks((nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL));
         hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
-                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge);
+                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
     } else {  // (not instantiated where the LDS form is used)
         constexpr int U = TeamShape<T, OP, P>::U;
-        size_t blocks = (nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U);
-        if (blocks == 0) blocks = 1;
+        const size_t blocks =
+            tl.blocks((nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U));
         hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
-                           dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge);
+                           dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
     }
     return hipGetLastError();
 }
 
 template <typename T, int OP>
 static hipError_t team_launch_op(int P, void *const *d, const void *const *sr, size_t n,
-                                 hipStream_t s)
+                                 Tiles tl, hipStream_t s)
 {
     switch (P) {
-    case 2: return team_launch_p<T, OP, 2>(d, sr, n, s);
-    case 3: return team_launch_p<T, OP, 3>(d, sr, n, s);
-    case 4: return team_launch_p<T, OP, 4>(d, sr, n, s);
-    case 5: return team_launch_p<T, OP, 5>(d, sr, n, s);
-    case 6: return team_launch_p<T, OP, 6>(d, sr, n, s);
-    case 7: return team_launch_p<T, OP, 7>(d, sr, n, s);
-    case 8: return team_launch_p<T, OP, 8>(d, sr, n, s);
+    case 2: return team_launch_p<T, OP, 2>(d, sr, n, tl, s);
+    case 3: return team_launch_p<T, OP, 3>(d, sr, n, tl, s);
+    case 4: return team_launch_p<T, OP, 4>(d, sr, n, tl, s);
+    case 5: return team_launch_p<T, OP, 5>(d, sr, n, tl, s);
+    case 6: return team_launch_p<T, OP, 6>(d, sr, n, tl, s);
+    case 7: return team_launch_p<T, OP, 7>(d, sr, n, tl, s);
+    case 8: return team_launch_p<T, OP, 8>(d, sr, n, tl, s);
     }
     return hipErrorInvalidValue;
 }
 
 #define TEAM_CASE(OPC)                                                         \
-    case OPC: return team_launch_op<T, OPC>(P, d, sr, n, s);
+    case OPC: return team_launch_op<T, OPC>(P, d, sr, n, tl, s);
 
 template <typename T>
 static hipError_t team_int(int op, int P, void *const *d, const void *const *sr, size_t n,
-                           hipStream_t s)
+                           Tiles tl, hipStream_t s)
 {
     switch (op) {
         TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD) TEAM_CASE(OP_AND) TEAM_CASE(OP_OR)
@@ -488,7 +504,7 @@ static hipError_t team_int(int op, int P, void *const *d, const void *const *sr,
 
 template <typename T>
 static hipError_t team_real(int op, int P, void *const *d, const void *const *sr, size_t n,
-                            hipStream_t s)
+                            Tiles tl, hipStream_t s)
 {
     switch (op) {
         TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD) TEAM_CASE(OP_MAX) TEAM_CASE(OP_MIN)
@@ -498,7 +514,7 @@ static hipError_t team_real(int op, int P, void *const *d, const void *const *sr
 
 template <typename T>
 static hipError_t team_cplx(int op, int P, void *const *d, const void *const *sr, size_t n,
-                            hipStream_t s)
+                            Tiles tl, hipStream_t s)
 {
     switch (op) {
         TEAM_CASE(OP_SUM) TEAM_CASE(OP_PROD)
@@ -506,23 +522,31 @@ static hipError_t team_cplx(int op, int P, void *const *d, const void *const *sr
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_team_tiles(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                             size_t n, int m, int k, hipStream_t s)
+{
+    if (P < 2 || P > kMaxTeam || m < 1 || k < 0 || k >= m) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    const Tiles tl{(unsigned) m, (unsigned) k};
+    switch (type) {
+    case T_SHORT: return team_int<int16_t>(op, P, dsts, srcs, n, tl, s);
+    case T_INT: return team_int<int32_t>(op, P, dsts, srcs, n, tl, s);
+    case T_LONG:
+    case T_LONGLONG: return team_int<int64_t>(op, P, dsts, srcs, n, tl, s);
+    case T_FLOAT: return team_real<float>(op, P, dsts, srcs, n, tl, s);
+    case T_DOUBLE: return team_real<double>(op, P, dsts, srcs, n, tl, s);
+    case T_COMPLEXF: return team_cplx<cfloat>(op, P, dsts, srcs, n, tl, s);
+    case T_COMPLEXD: return team_cplx<cdouble>(op, P, dsts, srcs, n, tl, s);
+    case T_LONGDOUBLE:
+        return m == 1 ? launch_team_longdouble(op, P, dsts, srcs, n, s) : hipErrorNotSupported;
+    }
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
                        size_t n, hipStream_t s)
 {
-    if (P < 2 || P > kMaxTeam) return hipErrorInvalidValue;
-    if (n == 0) return hipSuccess;
-    switch (type) {
-    case T_SHORT: return team_int<int16_t>(op, P, dsts, srcs, n, s);
-    case T_INT: return team_int<int32_t>(op, P, dsts, srcs, n, s);
-    case T_LONG:
-    case T_LONGLONG: return team_int<int64_t>(op, P, dsts, srcs, n, s);
-    case T_FLOAT: return team_real<float>(op, P, dsts, srcs, n, s);
-    case T_DOUBLE: return team_real<double>(op, P, dsts, srcs, n, s);
-    case T_COMPLEXF: return team_cplx<cfloat>(op, P, dsts, srcs, n, s);
-    case T_COMPLEXD: return team_cplx<cdouble>(op, P, dsts, srcs, n, s);
-    case T_LONGDOUBLE: return launch_team_longdouble(op, P, dsts, srcs, n, s);
-    }
-    return hipErrorInvalidValue;
+    return launch_team_tiles(type, op, P, dsts, srcs, n, 1, 0, s);
 }
 
 }  // namespace osgpu

@@ -10,6 +10,7 @@
  * Only the transport is replaced; the library under test is the product.
  */
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -29,9 +30,70 @@ static int g_npes = 0;
 static __thread int t_me = -1;
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 
+/* A polling barrier, as the reference's: its PEs spin on their pSync
+   (shmemc_wait_eq_until64 / _ne_until64, src/shmemc/barrier.c:32,47) rather
+   than sleep, and so does the multi-process runtime (pe_shm.c).  A sleeping
+   pthread barrier put a futex wake-up (5-20 us) into every call's timing.
+   Sense-reversing: the last arrival resets the count, then bumps gen.
+   PET_SLEEP_BARRIER=1: the sleeping form (mutex + condition variable), kept
+   for the A/B of tools/call_overhead.py. */
+typedef struct {
+    int size, count;
+    unsigned gen;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} spin_bar_t;
+
+static int sleep_barrier(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PET_SLEEP_BARRIER");
+        v = e && e[0] == '1';
+    }
+    return v;
+}
+
+static void spin_bar_init(spin_bar_t *b, int size)
+{
+    b->size = size;
+    b->count = 0;
+    b->gen = 0;
+    pthread_mutex_init(&b->mu, NULL);
+    pthread_cond_init(&b->cv, NULL);
+}
+
+static void spin_bar_wait(spin_bar_t *b)
+{
+    if (sleep_barrier()) {
+        pthread_mutex_lock(&b->mu);
+        const unsigned g = b->gen;
+        if (++b->count == b->size) {
+            b->count = 0;
+            __atomic_store_n(&b->gen, g + 1, __ATOMIC_RELEASE);
+            pthread_cond_broadcast(&b->cv);
+        } else {
+            while (b->gen == g) pthread_cond_wait(&b->cv, &b->mu);
+        }
+        pthread_mutex_unlock(&b->mu);
+        return;
+    }
+    const unsigned gen = __atomic_load_n(&b->gen, __ATOMIC_ACQUIRE);
+    if (__atomic_add_fetch(&b->count, 1, __ATOMIC_ACQ_REL) == b->size) {
+        __atomic_store_n(&b->count, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&b->gen, gen + 1, __ATOMIC_RELEASE);
+    } else {
+        unsigned spins = 0;
+        while (__atomic_load_n(&b->gen, __ATOMIC_ACQUIRE) == gen) {
+            __builtin_ia32_pause();
+            if (++spins > 4096) sched_yield();  /* more PE threads than cores */
+        }
+    }
+}
+
 typedef struct {
     int used, start, stride, size;
-    pthread_barrier_t b;
+    spin_bar_t b;
 } bar_t;
 static bar_t g_bars[MAXBAR];
 static long g_bar_calls[MAXPE];
@@ -49,10 +111,7 @@ int pet_init(int npes)
     if (npes < 1 || npes > MAXPE) return -1;
     pthread_mutex_lock(&g_mu);
     for (int i = 0; i < MAXBAR; i++)
-        if (g_bars[i].used) {
-            pthread_barrier_destroy(&g_bars[i].b);
-            g_bars[i].used = 0;
-        }
+        g_bars[i].used = 0;
     memset(g_bar_calls, 0, sizeof(g_bar_calls));
     memset(g_heap, 0, sizeof(g_heap));
     memset(g_heap_bytes, 0, sizeof(g_heap_bytes));
@@ -61,9 +120,9 @@ int pet_init(int npes)
     return 0;
 }
 
-static pthread_barrier_t *find_bar(int start, int stride, int size)
+static spin_bar_t *find_bar(int start, int stride, int size)
 {
-    pthread_barrier_t *r = NULL;
+    spin_bar_t *r = NULL;
     pthread_mutex_lock(&g_mu);
     for (int i = 0; i < MAXBAR && !r; i++)
         if (g_bars[i].used && g_bars[i].start == start && g_bars[i].stride == stride &&
@@ -75,7 +134,7 @@ static pthread_barrier_t *find_bar(int start, int stride, int size)
             g_bars[i].start = start;
             g_bars[i].stride = stride;
             g_bars[i].size = size;
-            pthread_barrier_init(&g_bars[i].b, NULL, (unsigned) size);
+            spin_bar_init(&g_bars[i].b, size);
             r = &g_bars[i].b;
         }
     pthread_mutex_unlock(&g_mu);
@@ -86,9 +145,9 @@ void pet_barrier(int PE_start, int logPE_stride, int PE_size, long *pSync)
 {
     (void) pSync; /* left at SHMEM_SYNC_VALUE, as the reference's barrier leaves it */
     if (t_me >= 0 && t_me < MAXPE) __atomic_add_fetch(&g_bar_calls[t_me], 1, __ATOMIC_RELAXED);
-    pthread_barrier_t *b = find_bar(PE_start, logPE_stride, PE_size);
+    spin_bar_t *b = find_bar(PE_start, logPE_stride, PE_size);
     if (!b) { fprintf(stderr, "pe_threads: barrier table full\n"); abort(); }
-    pthread_barrier_wait(b);
+    spin_bar_wait(b);
 }
 
 long pet_barrier_calls(int pe) { return (pe >= 0 && pe < MAXPE) ? g_bar_calls[pe] : -1; }
@@ -117,7 +176,7 @@ static pe_ops_t g_table = {pet_my_pe, pet_n_pes, pet_barrier, pet_getmem};
 
 /* ---- C-level timing of the API: npes pthreads each call fn (a
    shmem_<T>_<op>_to_all) `reps` times; PE 0 times each collective call from
-   a common start (pthread barrier) to its own return, after one warm-up. */
+   a common start (polling barrier) to its own return, after one warm-up. */
 typedef void (*to_all_fn)(void *, void *, int, int, int, int, void *, long *);
 /* shmem_collect/fcollect/alltoall<bits> and shmem_broadcast<bits> */
 typedef void (*coll_fn)(void *, const void *, size_t, int, int, int, long *);
@@ -127,7 +186,7 @@ typedef struct {
     to_all_fn fn;
     int npes, n, reps, me;
     void **tgt, **src, **psync;
-    pthread_barrier_t *bar;
+    spin_bar_t *bar;
     double *times;
     int kind;        /* 0 to_all, 1 collect-like, 2 broadcast */
     size_t nelems;   /* kinds 1, 2 */
@@ -150,7 +209,7 @@ static void *timing_body(void *p)
     char wrk[4096];
     t_me = a->me;
     for (int r = 0; r <= a->reps; r++) {
-        pthread_barrier_wait(a->bar);
+        spin_bar_wait(a->bar);
         double t0 = now_s();
         if (a->kind == 0)
             a->fn(a->tgt[a->me], a->src[a->me], a->n, 0, 0, a->npes, wrk, psync);
@@ -160,7 +219,7 @@ static void *timing_body(void *p)
         else
             ((bcast_fn) (void *) a->fn)(a->tgt[a->me], a->src[a->me], a->nelems, a->root, 0, 0,
                                         a->npes, psync);
-        pthread_barrier_wait(a->bar);
+        spin_bar_wait(a->bar);
         if (a->me == 0) a->times[r] = now_s() - t0;
     }
     return NULL;
@@ -176,8 +235,8 @@ static double time_calls(void *fn, int kind, int npes, void **tgt, void **src, v
                          int n, size_t nelems, int root, int reps)
 {
     if (npes < 1 || npes > MAXPE || reps < 1) return -1.0;
-    pthread_barrier_t bar;
-    pthread_barrier_init(&bar, NULL, (unsigned) npes);
+    spin_bar_t bar;
+    spin_bar_init(&bar, npes);
     double *times = calloc((size_t) reps + 1, sizeof(double));
     pthread_t th[MAXPE];
     timing_arg args[MAXPE];
@@ -187,7 +246,6 @@ static double time_calls(void *fn, int kind, int npes, void **tgt, void **src, v
         pthread_create(&th[i], NULL, timing_body, &args[i]);
     }
     for (int i = 0; i < npes; i++) pthread_join(th[i], NULL);
-    pthread_barrier_destroy(&bar);
     qsort(times + 1, (size_t) reps, sizeof(double), cmpd);
     double med = times[1 + reps / 2];
     free(times);

@@ -2,9 +2,13 @@
 """call_overhead.py -- where the whole-call time of the TEAM path goes
 (bench.py roofline_call: shmem_double_sum_to_all, 2 PEs as pthreads on one
 GPU, nreduce = 64 Mi, src/reductions.c:82,113 barriers), per completion-wait
-mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait).  (Round-4
-files _1.._4 also compare a merged launch of co-resident PE threads,
-OSGPU_TEAM_LOCAL_MERGE, since removed: it was no faster.)  Each mode
+mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait) and flags:
++contig (OSGPU_TEAM_LOCAL_TILES=0: contiguous shards for co-resident PE
+threads instead of interleaved tiles, shmem_reduce.cpp run_team), +sleep
+(PET_SLEEP_BARRIER=1: the PE-thread runtime's barrier sleeps instead of
+polling, tests/support/pe_threads.c).  (Round-4 files _1.._5 also compare a
+merged launch of co-resident PE threads and one shared stream, since
+removed: neither was faster.)  Each mode
 runs in its own process (the mode is read once) with OSGPU_CALL_TRACE=1:
 PE 0's host clock at entry sync, barrier 1, launch, completion wait,
 barrier 2; the median of every phase over the calls, beside the call time
@@ -61,15 +65,15 @@ def child(mode):
 
 def main():
     out = open(os.path.join(ROOT, "gpurun_out", "call_overhead.jsonl"), "a")
-    # MODE = <OSGPU_SYNC>[+nomerge]: +nomerge sets OSGPU_TEAM_LOCAL_MERGE=0
-    # (meaningful only for the round-4 builds that had the merged launch)
-    for mode in os.environ.get("CO_MODES", "block,word,block,word").split(","):
-        sync, _, extra = mode.partition("+")
+    # MODE = <OSGPU_SYNC>[+contig][+sleep]
+    default = "block+contig+sleep,block+contig,block,word"
+    for mode in os.environ.get("CO_MODES", default + "," + default).split(","):
+        sync, *flags = mode.split("+")
         env = dict(os.environ, OSGPU_SYNC=sync, OSGPU_CALL_TRACE="1")
-        if extra == "nomerge":
-            env["OSGPU_TEAM_LOCAL_MERGE"] = "0"
-        if extra == "shared":   # (r04_call_overhead_5: one team stream per
-            env["OSGPU_TEAM_STREAM"] = "shared"    # device, since removed)
+        if "contig" in flags:
+            env["OSGPU_TEAM_LOCAL_TILES"] = "0"
+        if "sleep" in flags:
+            env["PET_SLEEP_BARRIER"] = "1"
         r = subprocess.run([sys.executable, __file__, "child", mode], env=env, capture_output=True,
                            text=True, timeout=600)
         if r.returncode != 0:

@@ -35,7 +35,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     vmmprobe) step vmmprobe 200 python -u tools/vmm_probe.py 2 ;;
     vmm)   step vmm 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_multiproc.py -k vmm ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS} ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 20 --warmup 5 ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --no-extra --steps 20 --warmup 5 ;;
     tune)  step tune 300 ./tools/tune_combine ;;
     tunens) step tunens${TUNE_N}a${ALLOC}c${CHUNK} 300 ./tools/tune_ns ${TUNE_N:-134217728} ${TUNE_REPS:-20} ;;
     latency) step latency 300 python tools/latency_probe.py ;;
@@ -61,15 +61,15 @@ for s in ${STEPS:-smoke tests bench prof}; do
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
     multi8_self) step multi8_self 900 python bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     multi4_s) step multi4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 200 ;;
-    prof3) step prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
-    pmc3)  step pmc3f 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3f -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
-           step pmc3w 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc3w -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+    prof3) step prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
+    pmc3)  step pmc3f 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3f -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
+           step pmc3w 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc3w -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic.json &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team.json "team_vec_kernel<double, 0, 2, true>" 32 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team4.json "team_lds_kernel<double, 0, 4, true, 4" 64 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc3f gpurun_out/pmc3w $((64<<20)) gpurun_out/traffic_team8.json "team_vec_kernel<double, 0, 8, true>" 128 ;;
-    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
-           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --no-extra --steps 5 --warmup 2 &&
            python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $((64<<20)) gpurun_out/traffic.json &&
            python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $((64<<20)) gpurun_out/traffic_team.json "team_vec_kernel<double, 0, 2, true>" 32 ;;
   esac

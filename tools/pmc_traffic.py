@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py into HBM
-bytes per launch of the combine kernel (profiles/<round>_traffic.json).
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into HBM bytes per
+launch of one kernel (profiles/<round>_traffic*.json; bench.py's live
+traffic uses traffic() on its own passes over tools/pmc_probe.py).
 
 Corrections (MI355X_MICROARCH.md, section HBM / rocprofv3 PMC):
   * FETCH_SIZE and WRITE_SIZE are in KiB;
@@ -14,7 +15,7 @@ usage: pmc_traffic.py FETCH_DIR WRITE_DIR NREDUCE OUT.json [KERNEL [BYTES_PER_EL
   KERNEL          substring of the kernel name (default the K=2 double-sum
                   combine); BYTES_PER_ELEM algorithmic bytes per element per
                   launch (default 24 = 2 reads + 1 write of 8 B; the team
-                  kernel at P = 2: 32)
+                  kernel at P members: 16 * P)
 """
 import csv
 import glob
@@ -24,44 +25,48 @@ import statistics
 import sys
 
 KERNEL = "combine_vec_kernel<double, 0, 2>"
+METHOD = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 "
+          "(gfx950 half-count on 16-B streaming reads), KiB -> bytes, median over launches")
 
 
-def values(d, counter):
-    global KERNEL
+def values(d, counter, kernel=KERNEL):
     vals = []
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(p) as f:
             for row in csv.DictReader(f):
-                if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return vals
 
 
-def main():
-    global KERNEL
-    fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    if len(sys.argv) > 5:
-        KERNEL = sys.argv[5]
-    per_elem = int(sys.argv[6]) if len(sys.argv) > 6 else 24
-    f = values(fdir, "FETCH_SIZE")
-    w = values(wdir, "WRITE_SIZE")
+def traffic(fdir, wdir, n, kernel=KERNEL, per_elem=24):
+    """dict of the per-launch HBM bytes of `kernel`, or None without rows"""
+    f = values(fdir, "FETCH_SIZE", kernel)
+    w = values(wdir, "WRITE_SIZE", kernel)
     if not f or not w:
-        sys.exit(f"no counter rows for {KERNEL} (fetch {len(f)}, write {len(w)})")
+        return None
     fk, wk = statistics.median(f), statistics.median(w)
     read_b = 2.0 * fk * 1024.0
     write_b = wk * 1024.0
     alg = per_elem * n
-    res = {
-        "kernel": KERNEL, "nreduce": n, "launches": [len(f), len(w)],
+    return {
+        "kernel": kernel, "nreduce": n, "launches": [len(f), len(w)],
         "FETCH_SIZE_KiB_median": fk, "WRITE_SIZE_KiB_median": wk,
         "read_bytes": read_b, "write_bytes": write_b,
         "bytes_per_launch": read_b + write_b,
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg,
-        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
-                  "bench.py; FETCH_SIZE x2 (gfx950 half-count on 16-B streaming reads), "
-                  "KiB -> bytes",
+        "method": METHOD,
     }
+
+
+def main():
+    fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    kernel = sys.argv[5] if len(sys.argv) > 5 else KERNEL
+    per_elem = int(sys.argv[6]) if len(sys.argv) > 6 else 24
+    res = traffic(fdir, wdir, n, kernel, per_elem)
+    if res is None:
+        sys.exit(f"no counter rows for {kernel}")
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
     print(json.dumps(res))
