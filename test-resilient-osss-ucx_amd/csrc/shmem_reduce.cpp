@@ -124,7 +124,9 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
 // ~6 % longer than one full grid (profiles/r04_call_overhead_1..4.jsonl).
 // Calls on a set are matched by a per-thread sequence number: OpenSHMEM
 // members call a set's collectives in the same order.
-// OSGPU_TEAM_LOCAL_TILES=0: contiguous shards always.
+// OSGPU_TEAM_LOCAL: tiles (default) | merge (the run's first member
+// launches one grid over the whole run, the others only wait in the
+// barriers) | shards (contiguous shards always).
 struct LocalCall {
     unsigned mask = 0;  // active-set indices of the local members
     int left = 0;       // registered members not yet done
@@ -133,13 +135,16 @@ std::mutex g_local_mu;
 std::map<std::tuple<int, int, int, int, unsigned long long>, LocalCall> g_local;
 thread_local std::map<std::tuple<int, int, int, int>, unsigned long long> t_local_seq;
 
-bool local_tiles()
+enum { LOCAL_SHARDS = 0, LOCAL_TILES, LOCAL_MERGE };
+int local_mode()
 {
-    static const bool on = [] {
-        const char *e = getenv("OSGPU_TEAM_LOCAL_TILES");
-        return !(e && !strcmp(e, "0"));
+    static const int m = [] {
+        const char *e = getenv("OSGPU_TEAM_LOCAL");
+        if (e && !strcmp(e, "shards")) return (int) LOCAL_SHARDS;
+        if (e && !strcmp(e, "merge")) return (int) LOCAL_MERGE;
+        return (int) LOCAL_TILES;
     }();
-    return on;
+    return m;
 }
 
 void run_team(const Call &c, const std::vector<const void *> &srcs,
@@ -148,7 +153,9 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
     const int es = (int) (s > 16 ? 16 : s);
-    const bool tiles = local_tiles() && c.type != osgpu::T_LONGDOUBLE;
+    const int mode = local_mode();
+    // (long double: contiguous shards or merged runs, no tiles)
+    const bool tiles = mode == LOCAL_MERGE || (mode == LOCAL_TILES && c.type != osgpu::T_LONGDOUBLE);
     std::tuple<int, int, int, int, unsigned long long> key;
     if (tiles) {
         int dev = 0;
@@ -188,10 +195,15 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     }
     DBG("%s PE %d: team path, [%lld, %lld) of %d, tiles %d of %d, P=%d", c.name, c.me, lo, hi,
         c.nreduce, idx - first, last - first + 1, c.PE_size);
+    int m = last - first + 1, k = idx - first;
+    if (mode == LOCAL_MERGE) {
+        if (k > 0) hi = lo;  // the run's first member launches for all of it
+        m = 1;
+        k = 0;
+    }
     if (hi > lo) {
         hipError_t e = osgpu::launch_team_tiles(c.type, c.op, c.PE_size, dp.data(), sp.data(),
-                                                (size_t) (hi - lo), last - first + 1,
-                                                idx - first, st);
+                                                (size_t) (hi - lo), m, k, st);
         if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
     }
     call_trace(c.me, 3, "launch");
