@@ -56,6 +56,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
             python3 tools/ld_rocprof.py parse gpurun_out/ldprof gpurun_out/ldprof.log gpurun_out/ld_rocprof.json ;;
     callov) step callov 600 python -u tools/call_overhead.py ;;
     smallenv) step smallenv 600 python -u tools/small_call_env.py ;;
+    teamtlb) step teamtlb 300 rocprofv3 --pmc TCP_UTCL1_REQUEST TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_THRASHING_STALL -d gpurun_out/teamtlb -o run --output-format csv -- python3 tools/team_tlb_probe.py run &&
+             python3 tools/team_tlb_probe.py parse gpurun_out/teamtlb gpurun_out/teamtlb.log gpurun_out/team_tlb.jsonl ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
