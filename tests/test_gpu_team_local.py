@@ -1,8 +1,8 @@
 """The three ways PE threads that share one GPU split a team call
-(shmem_reduce.cpp run_team, OSGPU_TEAM_LOCAL): `tiles` (the default: member
-k of m folds tiles k, k + m, ... of the union of their shards) runs through
-every other GPU test; `shards` (contiguous shards) and `merge` (the run's
-first member launches one grid for all of it) are replayed here over every
+(shmem_reduce.cpp run_team, OSGPU_TEAM_LOCAL): `shards` (the default:
+contiguous shards) runs through every other GPU test; `tiles` (member k of
+m folds tiles k, k + m, ... of the union of their shards) and `merge` (the
+run's first member launches one grid for all of it) are replayed here over every
 golden case of tests/golden/reduce_cases.json, bit-exact against the
 reference's digests, each mode in its own process (the mode is read once
 per process)."""
@@ -40,7 +40,7 @@ print(json.dumps({"cases": n, "nbad": len(bad), "bad": bad[:5], "paths": paths})
 """
 
 
-@pytest.mark.parametrize("mode", ["shards", "merge"])
+@pytest.mark.parametrize("mode", ["tiles", "merge"])
 def test_team_local_modes_match_golden(mode):
     env = dict(os.environ, OSGPU_TEAM_LOCAL=mode)
     r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], env=env, capture_output=True,

@@ -3,9 +3,10 @@
 (bench.py roofline_call: shmem_double_sum_to_all, 2 PEs as pthreads on one
 GPU, nreduce = 64 Mi, src/reductions.c:82,113 barriers), per completion-wait
 mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait) and flags:
-+contig / +merge (OSGPU_TEAM_LOCAL=shards / merge: contiguous shards, or
-one grid launched by the first PE thread, instead of interleaved tiles for
-co-resident PE threads, shmem_reduce.cpp run_team), +sleep
++tiles / +merge (OSGPU_TEAM_LOCAL=tiles / merge: interleaved tiles, or one
+grid launched by the first PE thread, instead of contiguous shards for
+co-resident PE threads, shmem_reduce.cpp run_team; +contig = the default
+shards, spelled out), +sleep
 (PET_SLEEP_BARRIER=1: the PE-thread runtime's barrier sleeps instead of
 polling, tests/support/pe_threads.c).  (Round-4 files _1.._5 also compare a
 merged launch of co-resident PE threads and one shared stream, since
@@ -66,13 +67,15 @@ def child(mode):
 
 def main():
     out = open(os.path.join(ROOT, "gpurun_out", "call_overhead.jsonl"), "a")
-    # MODE = <OSGPU_SYNC>[+contig|+merge][+sleep]
-    default = "block+contig+sleep,block+contig,block,block+merge,word+merge"
+    # MODE = <OSGPU_SYNC>[+contig|+tiles|+merge][+sleep]
+    default = "block+contig+sleep,block+contig,block+tiles,block+merge,word+merge"
     for mode in os.environ.get("CO_MODES", default + "," + default).split(","):
         sync, *flags = mode.split("+")
         env = dict(os.environ, OSGPU_SYNC=sync, OSGPU_CALL_TRACE="1")
         if "contig" in flags:
             env["OSGPU_TEAM_LOCAL"] = "shards"
+        if "tiles" in flags:
+            env["OSGPU_TEAM_LOCAL"] = "tiles"
         if "merge" in flags:
             env["OSGPU_TEAM_LOCAL"] = "merge"
         if "sleep" in flags:
