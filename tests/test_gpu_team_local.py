@@ -40,9 +40,15 @@ print(json.dumps({"cases": n, "nbad": len(bad), "bad": bad[:5], "paths": paths})
 """
 
 
-@pytest.mark.parametrize("mode", ["tiles", "merge"])
+@pytest.mark.parametrize("mode", ["tiles", "merge", "merge+word"])
 def test_team_local_modes_match_golden(mode):
-    env = dict(os.environ, OSGPU_TEAM_LOCAL=mode)
+    # merge+word: also OSGPU_SYNC=word (completion by a host-mapped word the
+    # stream writes behind the kernel, runtime.cpp stream_wait), the fastest
+    # combination for PE threads sharing a GPU (profiles/r04_call_overhead_6.jsonl)
+    local, _, sync = mode.partition("+")
+    env = dict(os.environ, OSGPU_TEAM_LOCAL=local)
+    if sync:
+        env["OSGPU_SYNC"] = sync
     r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], env=env, capture_output=True,
                        text=True, timeout=280)
     assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
