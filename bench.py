@@ -814,8 +814,8 @@ def bench_single(args):
                 "bound": "hbm", "achieved": 4 * n * 8 / tcall / 1e9, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": 4 * n * 8 / tcall / 1e9 / HBM_PEAK_GBS,
                 "traffic": None, "ms_per_call": tcall * 1e3,
-                "team_local": os.environ.get("OSGPU_TEAM_LOCAL", "shards"),
-                "sync": os.environ.get("OSGPU_SYNC", "block"),
+                "team_local": os.environ.get("OSGPU_TEAM_LOCAL", "merge"),
+                "sync": os.environ.get("OSGPU_SYNC", "word"),
                 "what": "the whole shmem_double_sum_to_all call, 2 PEs (pthreads) on one GPU, "
                         "default (TEAM) path: entry sync, 2 barriers, both PEs' shard launches, "
                         "completion waits; 4*n*8 HBM bytes per call"}

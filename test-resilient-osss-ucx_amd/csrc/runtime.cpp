@@ -134,14 +134,19 @@ void entry_order(const char *where, hipStream_t st)
 }
 
 // Completion of our own stream.  OSGPU_SYNC:
-//   block (default)  hipStreamSynchronize (11.8 us launch-to-return for an
-//                    empty kernel, profiles/r01_overhead_probe.jsonl);
-//   spin             poll hipStreamQuery (13.5 us);
-//   word             hipStreamWriteValue64 of a sequence number into a
+//   word (default)   hipStreamWriteValue64 of a sequence number into a
 //                    host-mapped word behind the stream's work, the host
 //                    spinning on that word (an empty kernel's host-visible
 //                    word: 6.4 us); hipStreamQuery every 64 K spins turns a
-//                    faulted stream into an error instead of a hang.
+//                    faulted stream into an error instead of a hang.  The
+//                    reference's PEs poll too (shmemc_wait_*_until64).  A
+//                    2-PE 64 Mi-double team call: 369.6 us against 379-391
+//                    with `block` (profiles/r04_bench_merge_word.log,
+//                    r04_call_overhead_6.jsonl); 1 Ki ints with host
+//                    barriers 11.2 us against 15.4;
+//   block            hipStreamSynchronize (11.8 us launch-to-return for an
+//                    empty kernel, profiles/r01_overhead_probe.jsonl);
+//   spin             poll hipStreamQuery (13.5 us).
 // OSGPU_CALL_TRACE=1: host clock at each phase of a host-barrier call
 // (run_team), printed on stderr by PE 0 as "[osgpu call] <phase> <us> ..."
 void call_trace(int me, int phase, const char *label)
@@ -172,9 +177,9 @@ int sync_mode()
 {
     static const int m = [] {
         const char *e = getenv("OSGPU_SYNC");
+        if (e && !strcmp(e, "block")) return 0;
         if (e && !strcmp(e, "spin")) return 1;
-        if (e && !strcmp(e, "word")) return 2;
-        return 0;
+        return 2;
     }();
     return m;
 }
@@ -182,10 +187,23 @@ int sync_mode()
 struct DoneWord {
     volatile unsigned long long *h = nullptr;
     void *d = nullptr;
-    unsigned long long seq = 0;
+    unsigned long long seq = 0;  // the last value written (travels with the word)
     int device = -1;
 };
-thread_local DoneWord t_done;
+// Words of threads that exited, for reuse by new ones (PE threads come and
+// go; no HIP call at thread exit)
+std::mutex g_words_mu;
+std::vector<DoneWord> g_words_free;
+struct ThreadWord {
+    DoneWord w;
+    ~ThreadWord()
+    {
+        if (!w.h) return;
+        std::lock_guard<std::mutex> lk(g_words_mu);
+        g_words_free.push_back(w);
+    }
+};
+thread_local ThreadWord t_word;
 
 void stream_wait(const char *where, hipStream_t st)
 {
@@ -202,14 +220,29 @@ void stream_wait(const char *where, hipStream_t st)
     }
     int dev = 0;
     HIPCHK(where, hipGetDevice(&dev));
+    DoneWord &t_done = t_word.w;
     if (!t_done.h || t_done.device != dev) {  // one word per thread and device
-        void *h = nullptr;
-        HIPCHK(where, hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(where, hipHostGetDevicePointer(&t_done.d, h, 0));
-        t_done.h = static_cast<volatile unsigned long long *>(h);
-        *t_done.h = 0;
-        t_done.seq = 0;
-        t_done.device = dev;
+        bool reused = false;
+        {
+            std::lock_guard<std::mutex> lk(g_words_mu);
+            if (t_done.h) g_words_free.push_back(t_done);
+            for (size_t i = 0; i < g_words_free.size(); i++)
+                if (g_words_free[i].device == dev) {
+                    t_done = g_words_free[i];
+                    g_words_free.erase(g_words_free.begin() + (long) i);
+                    reused = true;
+                    break;
+                }
+        }
+        if (!reused) {
+            void *h = nullptr;
+            HIPCHK(where, hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(where, hipHostGetDevicePointer(&t_done.d, h, 0));
+            t_done.h = static_cast<volatile unsigned long long *>(h);
+            *t_done.h = 0;
+            t_done.seq = 0;
+            t_done.device = dev;
+        }
     }
     const unsigned long long want = ++t_done.seq;
     HIPCHK(where, hipStreamWriteValue64(st, t_done.d, want, 0));

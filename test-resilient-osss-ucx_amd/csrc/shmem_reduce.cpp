@@ -124,12 +124,12 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
 // ~6 % longer than one full grid (profiles/r04_call_overhead_1..4.jsonl).
 // Calls on a set are matched by a per-thread sequence number: OpenSHMEM
 // members call a set's collectives in the same order.
-// OSGPU_TEAM_LOCAL: shards (the default: contiguous shards always, the
-// form every round-4 measurement of roofline_call used) | tiles | merge
-// (the run's first member launches one grid over the whole run, the others
-// only wait in the barriers).  One bench run with tiles measured the call at
-// 0.682 of 8 TB/s (profiles/r04_bench_live_pmc.log) against 0.69-0.70 with
-// shards on other boxes: not enough to change the default.
+// OSGPU_TEAM_LOCAL: merge (the default: the run's first member launches one
+// grid over the whole run, the others only wait in the barriers) | shards
+// (contiguous shards always) | tiles.  A 2-PE 64 Mi-double call: merged
+// 379-384 us, 376.5-376.8 with OSGPU_SYNC=word, shards 377-391, tiles
+// 401-409 (profiles/r04_call_overhead_6.jsonl); merged + word in the bench
+// 0.726 of 8 TB/s (r04_bench_merge_word.log) against 0.68-0.71.
 struct LocalCall {
     unsigned mask = 0;  // active-set indices of the local members
     int left = 0;       // registered members not yet done
@@ -144,8 +144,8 @@ int local_mode()
     static const int m = [] {
         const char *e = getenv("OSGPU_TEAM_LOCAL");
         if (e && !strcmp(e, "tiles")) return (int) LOCAL_TILES;
-        if (e && !strcmp(e, "merge")) return (int) LOCAL_MERGE;
-        return (int) LOCAL_SHARDS;
+        if (e && !strcmp(e, "shards")) return (int) LOCAL_SHARDS;
+        return (int) LOCAL_MERGE;
     }();
     return m;
 }

@@ -1,8 +1,10 @@
 """The three ways PE threads that share one GPU split a team call
-(shmem_reduce.cpp run_team, OSGPU_TEAM_LOCAL): `shards` (the default:
-contiguous shards) runs through every other GPU test; `tiles` (member k of
-m folds tiles k, k + m, ... of the union of their shards) and `merge` (the
-run's first member launches one grid for all of it) are replayed here over every
+(shmem_reduce.cpp run_team, OSGPU_TEAM_LOCAL): `merge` (the default: the
+run's first member launches one grid for all of it) runs through every other
+GPU test; `shards` (contiguous shards), `tiles` (member k of m folds tiles
+k, k + m, ... of the union of their shards) and `merge` with the blocking
+completion wait (OSGPU_SYNC=block instead of the default word) are replayed
+here over every
 golden case of tests/golden/reduce_cases.json, bit-exact against the
 reference's digests, each mode in its own process (the mode is read once
 per process)."""
@@ -40,11 +42,10 @@ print(json.dumps({"cases": n, "nbad": len(bad), "bad": bad[:5], "paths": paths})
 """
 
 
-@pytest.mark.parametrize("mode", ["tiles", "merge", "merge+word"])
+@pytest.mark.parametrize("mode", ["shards", "tiles", "merge+block"])
 def test_team_local_modes_match_golden(mode):
-    # merge+word: also OSGPU_SYNC=word (completion by a host-mapped word the
-    # stream writes behind the kernel, runtime.cpp stream_wait), the fastest
-    # combination for PE threads sharing a GPU (profiles/r04_call_overhead_6.jsonl)
+    # +block: OSGPU_SYNC=block (hipStreamSynchronize) instead of the default
+    # completion word (runtime.cpp stream_wait)
     local, _, sync = mode.partition("+")
     env = dict(os.environ, OSGPU_TEAM_LOCAL=local)
     if sync:

@@ -3,10 +3,10 @@
 (bench.py roofline_call: shmem_double_sum_to_all, 2 PEs as pthreads on one
 GPU, nreduce = 64 Mi, src/reductions.c:82,113 barriers), per completion-wait
 mode (OSGPU_SYNC block / spin / word, runtime.cpp stream_wait) and flags:
-+tiles / +merge (OSGPU_TEAM_LOCAL=tiles / merge: interleaved tiles, or one
-grid launched by the first PE thread, instead of contiguous shards for
-co-resident PE threads, shmem_reduce.cpp run_team; +contig = the default
-shards, spelled out), +sleep
++contig / +tiles / +merge (OSGPU_TEAM_LOCAL=shards / tiles / merge:
+contiguous shards, interleaved tiles, or one grid launched by the first PE
+thread, for co-resident PE threads, shmem_reduce.cpp run_team; merge is the
+default since r04_call_overhead_6), +sleep
 (PET_SLEEP_BARRIER=1: the PE-thread runtime's barrier sleeps instead of
 polling, tests/support/pe_threads.c).  (Round-4 files _1.._5 also compare a
 merged launch of co-resident PE threads and one shared stream, since
