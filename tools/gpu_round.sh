@@ -58,6 +58,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smallenv) step smallenv 600 python -u tools/small_call_env.py ;;
     teamtlb) step teamtlb 300 rocprofv3 --pmc TCP_UTCL1_REQUEST TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_THRASHING_STALL -d gpurun_out/teamtlb -o run --output-format csv -- python3 tools/team_tlb_probe.py run &&
              python3 tools/team_tlb_probe.py parse gpurun_out/teamtlb gpurun_out/teamtlb.log gpurun_out/team_tlb.jsonl ;;
+    teamea) export TT_COUNTERS=TCC_EA0_RDREQ,TCC_EA0_WRREQ
+            step counters 120 rocprofv3 --list-avail &&
+            step teamea 300 rocprofv3 --pmc TCC_EA0_RDREQ TCC_EA0_WRREQ -d gpurun_out/teamea -o run --output-format csv -- python3 tools/team_tlb_probe.py run &&
+            python3 tools/team_tlb_probe.py parse gpurun_out/teamea gpurun_out/teamea.log gpurun_out/team_ea.jsonl ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;

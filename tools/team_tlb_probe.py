@@ -25,7 +25,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "test-resilient-osss-ucx_amd")]
 P, N, REPS = 8, 64 << 20, 5
 TRIALS = int(os.environ.get("TT_TRIALS", "6"))
-COUNTERS = ("TCP_UTCL1_REQUEST", "TCP_UTCL1_TRANSLATION_MISS", "TCP_UTCL1_THRASHING_STALL")
+# the counters of the pass (TT_COUNTERS=a,b,... for another set, e.g. the
+# L2's fabric requests TCC_EA0_RDREQ,TCC_EA0_WRREQ: step `teamea`)
+COUNTERS = tuple(os.environ.get(
+    "TT_COUNTERS", "TCP_UTCL1_REQUEST,TCP_UTCL1_TRANSLATION_MISS,TCP_UTCL1_THRASHING_STALL").split(","))
 
 
 def run():
