@@ -62,6 +62,9 @@ for s in ${STEPS:-smoke tests bench prof}; do
             step counters 120 rocprofv3 --list-avail &&
             step teamea 300 rocprofv3 --pmc TCC_EA0_RDREQ TCC_EA0_WRREQ -d gpurun_out/teamea -o run --output-format csv -- python3 tools/team_tlb_probe.py run &&
             python3 tools/team_tlb_probe.py parse gpurun_out/teamea gpurun_out/teamea.log gpurun_out/team_ea.jsonl ;;
+    teamstall) export TT_COUNTERS=TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum,TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum,TCC_EA0_WRREQ_STALL_sum,TCC_TOO_MANY_EA_WRREQS_STALL_sum
+            step teamstall 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum -d gpurun_out/teamstall -o run --output-format csv -- python3 tools/team_tlb_probe.py run &&
+            python3 tools/team_tlb_probe.py parse gpurun_out/teamstall gpurun_out/teamstall.log gpurun_out/team_stall.jsonl ;;
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
