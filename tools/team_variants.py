@@ -38,6 +38,8 @@ VARIANTS = {
     "perout": (None, ["-DOSGPU_TEAM_PEROUT=1", "-DOSGPU_TEAM_PIPE=0"]),
     "tree2": (None, ["-DOSGPU_TEAM_LDS_MIN_P=9"]),    # register form at every P
     "final": (None, []),                              # the tree's defaults
+    "final2": (None, []),                             # duplicate build (control)
+    "g8_4": (None, ["-DOSGPU_TEAM_G8=4"]),            # 8 members: all 4 x 8 vectors in flight
     # (a two-half LDS tile, OSGPU_TEAM_LDS_SPLIT, measured equal to one and
     # was removed: profiles/r04_team_place_4.jsonl)
     "lds8": (None, ["-DOSGPU_TEAM_LDS_MAX_P=8"]),      # LDS form at 3-8 members
