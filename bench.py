@@ -253,6 +253,27 @@ def _timer_sig(pet):
                                     ctypes.c_int]
 
 
+def dma_d2h_state(nbytes=64 << 20, reps=3):
+    """The DMA engine's device-to-host rate right now (best of `reps`
+    64-MiB copies into pinned memory): 56-57 GB/s when the GPU's power state
+    is up, 28-30 in the low state an idle box starts in (and drops back to
+    at times) -- the state the STAGED path's DMA legs would see
+    (tools/d2h_timeline.hip).  Reported beside the host-staged rates."""
+    import torch
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    del d, h
+    return {"dma_d2h_GBs": nbytes / best / 1e9, "low_state": nbytes / best / 1e9 < 40}
+
+
 def host_staged_time(n, reps=5, pes=2):
     """The reference's data placement: sources and targets in HOST symmetric
     heaps.  shmem_double_sum_to_all over a 2-PE set on one GPU (pthreads as
@@ -267,7 +288,10 @@ def host_staged_time(n, reps=5, pes=2):
     L.osgpu_finalize()
     P = pes
     out = {"note": f"{P} PEs (pthreads) on one GPU, host heaps, nreduce={n} doubles per PE; "
-                   f"PCIe bytes per call = {P}*{n}*8 H2D + {P}*{n}*8 D2H"}
+                   f"PCIe bytes per call = {P}*{n}*8 H2D + {P}*{n}*8 D2H",
+           "stage_copy": os.environ.get("OSGPU_STAGE_COPY", "dma"),
+           "copy_streams": os.environ.get("OSGPU_COPY_STREAMS", "prio"),
+           "dma_state": dma_d2h_state()}
     for pinned in (True, False):
         tm = T.Team(P, 2 * n * 8 + 8192, device=False)
         toff = (n * 8 + 4095) // 4096 * 4096

@@ -57,6 +57,10 @@ struct CopySeg {
     size_t bytes;
 };
 hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
+// One range between HBM and pinned host memory mapped into the GPU (either
+// side may be the host's device view): a fixed grid (OSGPU_HOST_COPY_GRID,
+// default 256 workgroups) sized for one PCIe link, not for HBM (copy.hip)
+hipError_t launch_host_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
 // <= 2 KiB of 8-byte words read with plain (L2-cached) loads into dst
 hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t s);
 

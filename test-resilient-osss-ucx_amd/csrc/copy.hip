@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "combine.hpp"
 
@@ -121,7 +122,68 @@ __global__ __launch_bounds__(kThreads) void probe_load_kernel(const unsigned lon
     if (threadIdx.x < words) dst[threadIdx.x] = src[threadIdx.x];
 }
 
+// One range across PCIe, device <-> pinned host memory mapped into the GPU
+// (the STAGED path's legs, shmem_reduce.cpp run_staged).  A fixed grid of
+// kHostGrid workgroups walks the range in tiles of kThreads * kU vectors,
+// every lane's kU loads in flight before its stores.  Why a kernel and not
+// the DMA engine: the engine's device-to-host rate follows the GPU's power
+// state -- 28.4-29.5 GB/s for the first second of an idle box and again at
+// random later, 56.6 once the state is up -- while this kernel's writes
+// hold 53.9-54.0 GB/s in both states, and a DMA read beside it 41.8-42.0
+// each way (tools/d2h_timeline.hip, profiles/r05_dma_state_timeline.jsonl).
+// Vectors are aligned on the destination; block 0 copies the head and the
+// tail bytes.
+__global__ __launch_bounds__(kThreads) void host_copy_kernel(const char *__restrict__ s,
+                                                             char *__restrict__ d, size_t bytes)
+{
+    size_t head = (size_t) ((0 - (uintptr_t) d) & 15);
+    if (head > bytes) head = bytes;
+    const size_t nvec = (bytes - head) / 16;
+    const size_t tail0 = head + nvec * 16;
+    if (blockIdx.x == 0) {
+        const unsigned x = threadIdx.x;
+        if (x < head) d[x] = s[x];
+        if (x < bytes - tail0) d[tail0 + x] = s[tail0 + x];
+    }
+    const u32x4_a4 *sv = reinterpret_cast<const u32x4_a4 *>(s + head);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(d + head);
+    const size_t stride = (size_t) gridDim.x * kThreads * kU;
+    for (size_t base = (size_t) blockIdx.x * kThreads * kU + threadIdx.x; base < nvec;
+         base += stride) {
+        u32x4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const size_t i = base + (size_t) u * kThreads;
+            if (i < nvec) v[u] = __builtin_nontemporal_load(sv + i);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const size_t i = base + (size_t) u * kThreads;
+            if (i < nvec) dv[i] = v[u];
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_host_copy(void *dst, const void *src, size_t bytes, hipStream_t stream)
+{
+    static const unsigned grid = [] {
+        const char *e = getenv("OSGPU_HOST_COPY_GRID");
+        const long v = e ? atol(e) : 256;
+        return (unsigned) (v < 1 ? 1 : (v > 4096 ? 4096 : v));
+    }();
+    if (bytes == 0) return hipSuccess;
+    if (((uintptr_t) src ^ (uintptr_t) dst) & 3) {  // byte phases differ: the byte kernel
+        CopySeg g = {src, dst, bytes};
+        return launch_copy(&g, 1, stream);
+    }
+    const size_t tiles = (bytes + kBlockBytes - 1) / kBlockBytes;
+    hipLaunchKernelGGL(host_copy_kernel, dim3((unsigned) (tiles < grid ? tiles : grid)),
+                       dim3(kThreads), 0, stream, static_cast<const char *>(src),
+                       static_cast<char *>(dst), bytes);
+    return hipGetLastError();
+}
 
 hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t stream)
 {

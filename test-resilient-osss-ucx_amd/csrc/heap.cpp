@@ -736,7 +736,7 @@ extern "C" int osgpu_heap_destroy(void *base)
 // barrier returns (shmemc_quiet -> ucp_worker_flush ahead of the barrier,
 // src/shmemc/comms.c:147-161, src/shmemc/barrier.c:176-181).
 //
-// Test hook: OSGPU_PREFLIGHT_FAULT=<pe>:<peer> makes PE <pe> reach peer
+// Test hook: osgpu_test_preflight_fault(pe, peer) makes PE <pe> reach peer
 // <peer>'s heap chunks and staging through ANOTHER member's mappings (a
 // planted wrong mapping), which both legs must report.
 // ---------------------------------------------------------------------
@@ -774,14 +774,15 @@ void wpattern(unsigned long long *w, int writer, int owner, int region, int chun
     pattern(w, 2, writer, region + 8 * leg, (chunk << 12) ^ owner, end);
 }
 
-// OSGPU_PREFLIGHT_FAULT=<pe>:<peer> (test hook): the active-set index whose
-// mappings PE `me_pe` uses for member index i
+// planted by osgpu_test_preflight_fault (test hook; never from the
+// environment, so a stray variable cannot redirect real remote writes)
+std::atomic<int> g_fault_pe{-1}, g_fault_peer{-1};
+
+// the active-set index whose mappings PE `me` uses for member index i
 int probe_view(const Coll &c, int me, int i)
 {
-    const char *e = getenv("OSGPU_PREFLIGHT_FAULT");
-    int fpe = -1, fpeer = -1;
-    if (!e || sscanf(e, "%d:%d", &fpe, &fpeer) != 2 || fpe != c.me || fpeer != c.pe_at(i))
-        return i;
+    const int fpe = g_fault_pe.load(), fpeer = g_fault_peer.load();
+    if (fpe < 0 || fpe != c.me || fpeer != c.pe_at(i)) return i;
     for (int j = 0; j < c.PE_size; j++)
         if (j != i && j != me) return j;
     return me;  // two members: my own range stands in for the peer's
@@ -929,7 +930,9 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
     // 3. remote writes: 16 B per writer in 128-B blocks at both ends of every
     // heap chunk and of the staging area (what team.hip's stores into the
     // members' targets and the push form's inbox scatter do)
-    constexpr size_t WB = 16 * osgpu::kMaxTeam;
+    // 16 B per member, whole 128-B lines: sized by the active set, which may
+    // exceed the team kernel's kMaxTeam (staging and PE threads allow more)
+    const size_t WB = ((size_t) 16 * PE_size + 127) / 128 * 128;
     struct WBlock {
         const char *region;
         int chunk, end;
@@ -979,7 +982,8 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
     int nwrite = 0, nwbad = 0;
     if (!mine.empty() || H || S) {
         // 3a. clear my blocks and pull them into my L2
-        unsigned long long got[WB / 8];
+        std::vector<unsigned long long> gotv(WB / 8);
+        unsigned long long *got = gotv.data();
         for (const WBlock &b : mine) {
             (void) hipMemset(b.at, 0, WB);
             (void) hipDeviceSynchronize();
@@ -1069,4 +1073,20 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
         set_err("%s: %d of %d read probes and %d remote-write checks failed", where, nbad, nprobes,
                 nwbad);
     return all ? OSGPU_OK : OSGPU_EPEER;
+}
+
+// Test hook (tests/support/mp_worker.py): plant a wrong mapping for the next
+// osgpu_preflight calls of this process -- PE `pe` reaches peer `peer`
+// through another member's ranges.  (-1, -1) clears it.  Logged, so a
+// planted fault never goes unseen.
+extern "C" int osgpu_test_preflight_fault(int pe, int peer)
+{
+    if ((pe < 0) != (peer < 0)) return OSGPU_EINVAL;
+    g_fault_pe.store(-1);
+    g_fault_peer.store(peer);
+    g_fault_pe.store(pe);
+    if (pe >= 0)
+        fprintf(stderr, "[osgpu] test hook: preflight of PE %d reaches PE %d through another "
+                        "member's mappings\n", pe, peer);
+    return OSGPU_OK;
 }

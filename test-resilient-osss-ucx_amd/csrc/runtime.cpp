@@ -8,6 +8,7 @@
 
 #include <dlfcn.h>
 #include <stdarg.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -249,6 +250,11 @@ void stream_wait(const char *where, hipStream_t st)
     for (unsigned long spins = 1;; spins++) {
         if (*t_done.h >= want) return;
         __builtin_ia32_pause();
+        // past ~4 K spins (tens of us) give the core away now and then, like
+        // the PE-thread barrier (tests/support/pe_threads.c): with more PE
+        // threads than cores, spinning here must not starve the members this
+        // call is waiting for
+        if (spins > 4096 && (spins & 15) == 0) sched_yield();
         if ((spins & 0xffff) == 0) {
             e = hipStreamQuery(st);
             if (e == hipSuccess) {  // the write is behind everything: it must show
@@ -470,7 +476,7 @@ void *host_stage(const char *where, int me, size_t bytes)
         if (x.hstage) HIPCHK(where, hipHostFree(x.hstage));
         x.hstage = nullptr;
         x.hstage_bytes = 0;
-        HIPCHK(where, hipHostMalloc(&x.hstage, bytes, hipHostMallocDefault));
+        HIPCHK(where, hipHostMalloc(&x.hstage, bytes, hipHostMallocMapped));
         x.hstage_bytes = bytes;
     }
     return x.hstage;
@@ -738,13 +744,77 @@ bool map_members(const Coll &c, char *local, size_t bytes, std::vector<char *> &
 // same pair instead of competing.
 std::map<int, std::pair<hipStream_t, hipStream_t>> g_copy_streams;
 
+// The H2D and D2H copy streams must never share a hardware queue: HIP
+// gives a process GPU_MAX_HW_QUEUES queues per priority level (4 on the
+// pool) and deals further streams onto them, so with one more stream in the
+// process than the staging set expects (a torch side stream, the thread's
+// osgpu_combine stream) the D2H copies queued behind the H2D ones on one
+// queue -- the two directions took turns: 27.7 GB/s each way instead of
+// 44.5, and pageable 25 instead of 38-41 (tools/host_staged_context.py,
+// profiles/r05_host_staged_streams.jsonl; the round-3 regression of
+// BENCH_r03/r04).  Streams of different priorities come from different
+// queue pools, so H2D takes the lowest priority and D2H the highest: never
+// one queue, whatever else the process created.  (OSGPU_COPY_STREAMS=plain
+// restores default-priority streams, cumask gives each its own CU-masked
+// queue; both measured in that file.)
+extern "C" int osgpu_copy_stream_priorities(int least, int greatest, int *in, int *out)
+{
+    if (!in || !out) return OSGPU_EINVAL;
+    *in = least;
+    *out = greatest;
+    return least != greatest ? OSGPU_OK : OSGPU_EINVAL;  // one level: no separate pools
+}
+
+static void create_copy_stream(const char *where, int dev, hipStream_t *s, bool out)
+{
+    const char *e = getenv("OSGPU_COPY_STREAMS");
+    const bool plain = e && !strcmp(e, "plain");
+    bool cumask = e && !strcmp(e, "cumask");
+    if (!plain && !cumask) {
+        int least = 0, greatest = 0, pin = 0, pout = 0;
+        HIPCHK(where, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        if (osgpu_copy_stream_priorities(least, greatest, &pin, &pout) == OSGPU_OK) {
+            HIPCHK(where, hipStreamCreateWithPriority(s, hipStreamNonBlocking, out ? pout : pin));
+            return;
+        }
+        cumask = true;  // a single priority level: a queue of its own instead
+    }
+    if (cumask) {
+        int ncu = 0;
+        HIPCHK(where, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; i++) mask[i / 32] |= 1u << (i % 32);
+        HIPCHK(where, hipExtStreamCreateWithCUMask(s, (uint32_t) mask.size(), mask.data()));
+        return;
+    }
+    HIPCHK(where, hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+}
+
+// the priorities of this device's staging copy streams (tests)
+extern "C" int osgpu_copy_stream_info(int dev, int *in_prio, int *out_prio)
+{
+    hipStream_t a = nullptr, b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_copy_streams.find(dev);
+        if (it == g_copy_streams.end()) return OSGPU_EINVAL;
+        a = it->second.first;
+        b = it->second.second;
+    }
+    if (hipStreamGetPriority(a, in_prio) != hipSuccess || hipStreamGetPriority(b, out_prio) != hipSuccess) {
+        (void) hipGetLastError();
+        return OSGPU_EHIP;
+    }
+    return OSGPU_OK;
+}
+
 void device_copy_streams(const char *where, int dev, hipStream_t *in, hipStream_t *out)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     auto &p = g_copy_streams[dev];
     if (!p.first) {
-        HIPCHK(where, hipStreamCreateWithFlags(&p.first, hipStreamNonBlocking));
-        HIPCHK(where, hipStreamCreateWithFlags(&p.second, hipStreamNonBlocking));
+        create_copy_stream(where, dev, &p.first, false);
+        create_copy_stream(where, dev, &p.second, true);
     }
     *in = p.first;
     *out = p.second;

@@ -122,8 +122,10 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
 // GPU; with contiguous shards the two concurrent half-grids of a 2-PE call
 // streamed two distant ranges and ended ~16 us apart, the whole call taking
 // ~6 % longer than one full grid (profiles/r04_call_overhead_1..4.jsonl).
-// Calls on a set are matched by a per-thread sequence number: OpenSHMEM
-// members call a set's collectives in the same order.
+// Calls on a set are matched by a sequence number kept per (set, device,
+// PE) in this process -- not per OS thread, so a PE whose calls move
+// between threads (a thread pool) keeps its count: OpenSHMEM members call
+// a set's collectives in the same order.
 // OSGPU_TEAM_LOCAL: merge (the default: the run's first member launches one
 // grid over the whole run, the others only wait in the barriers) | shards
 // (contiguous shards always) | tiles.  A 2-PE 64 Mi-double call: merged
@@ -136,7 +138,7 @@ struct LocalCall {
 };
 std::mutex g_local_mu;
 std::map<std::tuple<int, int, int, int, unsigned long long>, LocalCall> g_local;
-thread_local std::map<std::tuple<int, int, int, int>, unsigned long long> t_local_seq;
+std::map<std::tuple<int, int, int, int, int>, unsigned long long> g_local_seq;  // + PE
 
 enum { LOCAL_SHARDS = 0, LOCAL_TILES, LOCAL_MERGE };
 int local_mode()
@@ -164,8 +166,9 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
         int dev = 0;
         HIPCHK(c.name, hipGetDevice(&dev));
         const auto set = std::make_tuple(c.PE_start, c.step, c.PE_size, dev);
-        key = std::tuple_cat(set, std::make_tuple(++t_local_seq[set]));
         std::lock_guard<std::mutex> lk(g_local_mu);
+        const unsigned long long seq = ++g_local_seq[std::tuple_cat(set, std::make_tuple(c.me))];
+        key = std::tuple_cat(set, std::make_tuple(seq));
         LocalCall &L = g_local[key];
         L.mask |= 1u << idx;
         L.left++;
@@ -489,6 +492,44 @@ void run_rccl(const Call &c)
     }
 }
 
+// How the STAGED path moves its chunks across PCIe (OSGPU_STAGE_COPY):
+//   dma (default)   both legs by the DMA engines (hipMemcpyAsync on the two
+//                   copy streams, runtime.cpp device_copy_streams): 44.5 GB/s
+//                   each way pinned, 38-41 pageable, 2 PEs at 64 Mi doubles;
+//   kout            H2D by DMA, D2H by launch_host_copy (a kernel writing
+//                   the host's device view); 34.7 pinned;
+//   kernel          both legs by kernel; 30.6-31.0 pinned
+//   (profiles/r05_staged_copy_modes.jsonl).  The kernel legs exist for the
+//   GPU's low power state, in which the DMA engine's D2H rate falls to
+//   28-30 GB/s (the first second of an idle box) while a kernel's writes
+//   hold 54 (tools/d2h_timeline.hip, profiles/r05_dma_state_timeline.jsonl);
+//   the bench reports that state beside the rates (dma_state).
+// A leg whose host memory has no device view takes the DMA engine.
+enum { STAGE_DMA = 0, STAGE_KOUT, STAGE_KERNEL };
+int stage_copy_mode()  // read per call (tests switch it between calls)
+{
+    const char *e = getenv("OSGPU_STAGE_COPY");
+    if (e && !strcmp(e, "kout")) return STAGE_KOUT;
+    if (e && !strcmp(e, "kernel")) return STAGE_KERNEL;
+    return STAGE_DMA;
+}
+
+// one staged leg: a kernel over the host side's device view (dview) when
+// the mode asks for one and the view exists, else the DMA engine
+void stage_leg(const char *name, int mode, void *dst, const void *src, size_t bytes,
+               bool to_host, const void *dview, hipStream_t st)
+{
+    const bool kern = dview && (mode == STAGE_KERNEL || (mode == STAGE_KOUT && to_host));
+    hipError_t e;
+    if (kern)
+        e = to_host ? osgpu::launch_host_copy(const_cast<void *>(dview), src, bytes, st)
+                    : osgpu::launch_host_copy(dst, dview, bytes, st);
+    else
+        e = hipMemcpyAsync(dst, src, bytes, to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice,
+                           st);
+    if (e != hipSuccess) fatal(name, "staging copy: %s", hipGetErrorString(e));
+}
+
 void run_staged(const Call &c, StageSet &S)
 {
     const size_t s = type_size(c.type);
@@ -512,6 +553,19 @@ void run_staged(const Call &c, StageSet &S)
                        ? (char *) host_stage(c.name, c.me, 4 * S.slot) : nullptr;
     auto bin = [&](int sl) { return bounce + (size_t) sl * S.slot; };
     auto bout = [&](int sl) { return bounce + (size_t) (2 + sl) * S.slot; };
+    // the GPU's view of the host side of each leg (null: DMA engine)
+    const int cmode = stage_copy_mode();
+    char *bounce_dev = nullptr;
+    if (bounce && cmode != STAGE_DMA &&
+        hipHostGetDevicePointer((void **) &bounce_dev, bounce, 0) != hipSuccess) {
+        (void) hipGetLastError();
+        bounce_dev = nullptr;
+    }
+    auto view = [&](const char *h, bool is_bounce, size_t n) -> const void * {
+        if (cmode == STAGE_DMA) return nullptr;
+        if (is_bounce) return bounce_dev ? bounce_dev + (h - bounce) : nullptr;
+        return host_device_view(h, n);
+    };
     auto chunk_n = [&](size_t ch) { return (ch + 1) * C <= N ? C : N - ch * C; };
     // D2H of chunk ch landed in bout: copy it to the caller's array
     auto drain = [&](size_t ch) {
@@ -525,8 +579,8 @@ void run_staged(const Call &c, StageSet &S)
             par_memcpy(bin((int) (ch & 1)), from, n * s);
             from = bin((int) (ch & 1));
         }
-        HIPCHK(c.name, hipMemcpyAsync(S.in(idx, ch & 1), from, n * s, hipMemcpyHostToDevice,
-                                      S.st_in));
+        stage_leg(c.name, cmode, S.in(idx, ch & 1), from, n * s, false, view(from, bounce_in, n * s),
+                  S.st_in);
         HIPCHK(c.name, hipEventRecord(S.ev_in[ch & 1], S.st_in));
     };
     entry_sync(c.name);
@@ -567,8 +621,8 @@ void run_staged(const Call &c, StageSet &S)
         }
         stream_wait(c.name, S.st_c);
         barrier(c);  // every shard of my out[sl] written
-        HIPCHK(c.name, hipMemcpyAsync(bounce_out ? bout(sl) : result + ch * C * s,
-                                      S.out(idx, sl), n * s, hipMemcpyDeviceToHost, S.st_out));
+        char *to = bounce_out ? bout(sl) : result + ch * C * s;
+        stage_leg(c.name, cmode, to, S.out(idx, sl), n * s, true, view(to, bounce_out, n * s), S.st_out);
         HIPCHK(c.name, hipEventRecord(S.ev_out[sl], S.st_out));
     }
     stream_wait(c.name, S.st_out);

@@ -250,14 +250,53 @@ def preflight_mode(L, PES, rank, world):
     dist.barrier()
     # a planted wrong mapping (heap.cpp test hook): PE 0 reaches PE 1's heap
     # chunks and staging through PE 2's ranges
-    os.environ["OSGPU_PREFLIGHT_FAULT"] = "0:1"
+    assert L.osgpu_test_preflight_fault(0, 1) == 0
     rc_fault, rep_fault = osgpu.preflight(base, 0, 0, world, psync)
-    del os.environ["OSGPU_PREFLIGHT_FAULT"]
+    assert L.osgpu_test_preflight_fault(-1, -1) == 0
     dist.barrier()
     assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
     return {"preflight_rc": rc, "preflight": rep, "preflight_none_rc": rc_none,
             "preflight_none": rep_none, "after_exact": exact, "after_path": ran,
             "fault_rc": rc_fault, "fault": rep_fault}
+
+
+def preflight_wide_mode(L, PES, rank, world):
+    """osgpu_preflight over an active set larger than the team kernel's 8
+    members (the remote-write blocks were sized for 8 writers):
+    a 2-chunk heap, the staging areas and the flag areas; every probe of
+    every peer must pass, and the heap's chunk ends outside the written
+    blocks must keep their bytes (nothing written past a block)."""
+    import torch
+    torch.cuda.set_device(0)
+    psync = PES.pes_heap(rank) + PES.pes_heap_bytes() - 8192
+    bp = ctypes.c_void_p()
+    chunk = 64 << 20
+    assert L.osgpu_heap_create(2 * chunk, 0, 0, world, psync, ctypes.byref(bp)) == 0, \
+        L.osgpu_last_error().decode()
+    base = bp.value
+    # a guard band next to each block: 4 KiB below every high-end block and
+    # above every low-end block, filled with a known byte
+    wb = (16 * world + 127) // 128 * 128
+    guard = torch.full((4096,), 0xA5, dtype=torch.uint8, device="cuda:0")
+    spots = [base + wb, base + chunk - wb - 4096, base + chunk + wb,
+             base + 2 * chunk - wb - 4096]
+    for a in spots:
+        osgpu.copy([a], [guard.data_ptr()], [4096])
+    torch.cuda.synchronize()
+    dist.barrier()
+    rc, rep = osgpu.preflight(base, 0, 0, world, psync)
+    rc_none, rep_none = osgpu.preflight(None, 0, 0, world, psync)
+    torch.cuda.synchronize()
+    back = torch.empty(4096, dtype=torch.uint8, device="cuda:0")
+    intact = True
+    for a in spots:
+        osgpu.copy([back.data_ptr()], [a], [4096])
+        torch.cuda.synchronize()
+        intact = intact and bool(torch.equal(back, guard))
+    dist.barrier()
+    assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
+    return {"preflight_rc": rc, "preflight": rep, "preflight_none_rc": rc_none,
+            "preflight_none": rep_none, "guards_intact": intact}
 
 
 def mixed_topology_mode(L, rank, world):
@@ -1105,7 +1144,7 @@ def main():
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
             "hoststaged", "hostcoll", "golden", "goldenhost", "collgolden", "latency",
             "timeout", "vmm", "late", "mixpush", "heapcycle", "finalizecycle", "heapleak",
-            "fuzz", "preflight"):
+            "fuzz", "preflight", "preflightwide"):
         from support import peshm
         PES = peshm.init(rank, world, (1 << 26) if mode == "goldenhost" else (1 << 24), dist)
         assert L.osgpu_set_pe_ops(PES.pes_ops()) == 0
@@ -1170,6 +1209,8 @@ def main():
         res.update(heap_leak_mode(L, PES, rank, world))
     if mode == "preflight":
         res.update(preflight_mode(L, PES, rank, world))
+    if mode == "preflightwide":
+        res.update(preflight_wide_mode(L, PES, rank, world))
     if mode == "mixedtopo":
         res.update(mixed_topology_mode(L, rank, world))
     if mode == "finalizecycle":

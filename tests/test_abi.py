@@ -195,6 +195,23 @@ def test_fold_order_matches_reference_walk(lib):
         osgpu.fold_order(1, 0, 1, 2)   # PE 1 is not in {0, 2}
 
 
+def test_copy_streams_come_from_different_queue_pools(lib):
+    """The STAGED path's H2D and D2H streams take the lowest and the highest
+    stream priority: HIP pools hardware queues per priority level, so the
+    two directions never share a queue (sharing one, they took turns: 27.7
+    GB/s each way instead of 44.5 -- the round-3 host-staged regression,
+    profiles/r05_host_staged_streams.jsonl).  ROCm's range is (0, -1) on
+    this image; a one-level range is refused (the library then gives each
+    stream a CU-masked queue of its own)."""
+    i, o = ctypes.c_int(7), ctypes.c_int(7)
+    for least, greatest in ((0, -1), (1, -1), (0, -2)):
+        assert lib.osgpu_copy_stream_priorities(least, greatest, ctypes.byref(i),
+                                                ctypes.byref(o)) == 0
+        assert (i.value, o.value) == (least, greatest) and i.value != o.value
+    assert lib.osgpu_copy_stream_priorities(0, 0, ctypes.byref(i), ctypes.byref(o)) != 0
+    assert lib.osgpu_copy_stream_priorities(0, -1, None, None) != 0
+
+
 @pytest.mark.parametrize("eb", [2, 4, 8, 16])
 def test_shard_ranges_partition(lib, eb):
     for n in (0, 1, 7, 63, 64, 65, 1000, 4097, 1 << 20, (1 << 20) + 3):

@@ -183,6 +183,73 @@ def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
     osgpu.load().osgpu_finalize()
 
 
+@pytest.mark.parametrize("stage_copy", ["kout", "kernel", "dma"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_staged_copy_modes(torch_cuda, stage_copy, pinned, monkeypatch):
+    """The STAGED path's PCIe legs by DMA engine or by kernel
+    (OSGPU_STAGE_COPY, shmem_reduce.cpp stage_leg), on pageable heaps (the
+    pinned bounce buffers' device view) and on heaps pinned with
+    osgpu_host_register (the heap's own device view), 4 KiB chunks, odd
+    lengths and offsets: bit-exact on the golden cases."""
+    monkeypatch.setenv("OSGPU_STAGE_BYTES", "4096")
+    monkeypatch.setenv("OSGPU_HOST_PATH", "staged")
+    monkeypatch.setenv("OSGPU_STAGE_COPY", stage_copy)
+    L = osgpu.load()
+    L.osgpu_finalize()
+    tm = team(device=False)
+    if pinned:
+        assert L.osgpu_host_register(ctypes.c_void_p(tm.base), tm.npes * tm.H) == 0
+        L.osgpu_set_fused_max_bytes(0)   # small calls too: the staged path
+    try:
+        n = 0
+        for c in CASES:
+            if (c["type"], c["op"]) in (("double", "sum"), ("int", "xor"), ("complexd", "prod"),
+                                        ("short", "min"), ("longdouble", "max")) and \
+                    c["nreduce"] <= 4097 and c["npes"] in (2, 3, 8):
+                check(c, run_case(tm, c))
+                if c["nreduce"] > 0:
+                    assert tm.last_paths[c["PE_start"]] == "staged", tm.last_paths
+                n += 1
+        assert n > 20
+    finally:
+        if pinned:
+            L.osgpu_set_fused_max_bytes(-1)
+            L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
+        L.osgpu_finalize()
+
+
+def test_staged_copy_streams_survive_extra_streams(torch_cuda):
+    """With more streams in the process than the staging set expects (a
+    torch side stream and the thread's osgpu stream, created first), the
+    H2D and D2H copy streams still come from different priority pools, and
+    a 64 Mi-double pinned STAGED call keeps both directions moving at once:
+    more than 36 GB/s each way (27.7 when they shared a queue and took
+    turns), unless the GPU's DMA engine is in its low power state (then
+    its D2H alone is below 40 GB/s and the rate is not asserted)."""
+    import torch
+    import bench
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.ones(1 << 20, device="cuda").add_(1)
+    osgpu.load().osgpu_get_stream()
+    torch.cuda.synchronize()
+    res = bench.host_staged_time(64 << 20, reps=3)
+    L = osgpu.load()
+    dev = torch.cuda.current_device()
+    assert res["pinned"]["correct"] and res["pageable"]["correct"], res
+    # (host_staged_time finalizes at its end: set the streams up again)
+    tm = team(device=False)
+    c = next(c for c in CASES if c["type"] == "double" and c["op"] == "sum" and c["npes"] == 2
+             and c["nreduce"] > 1000)
+    check(c, run_case(tm, c))
+    pi, po = ctypes.c_int(), ctypes.c_int()
+    assert L.osgpu_copy_stream_info(dev, ctypes.byref(pi), ctypes.byref(po)) == 0
+    assert pi.value != po.value, (pi.value, po.value)
+    if not res["dma_state"]["low_state"]:
+        assert res["pinned"]["pcie_GBs_each_way"] > 36, res
+    del side
+
+
 _S = []
 
 

@@ -398,7 +398,7 @@ def test_preflight_processes(tmp_path, monkeypatch):
     and copy kernel), and every peer's remote writes into this process's
     chunk ends and staging area (host copy, then copy kernel) reach it; a
     reduction on the same heap afterwards is bit-exact.  A planted wrong
-    mapping (OSGPU_PREFLIGHT_FAULT=0:1: PE 0 reaches PE 1 through PE 2's
+    mapping (osgpu_test_preflight_fault(0, 1): PE 0 reaches PE 1 through PE 2's
     ranges) fails PE 0's reads of PE 1 and PE 1's check of PE 0's writes."""
     import torch
     if not torch.cuda.is_available():
@@ -428,6 +428,27 @@ def test_preflight_processes(tmp_path, monkeypatch):
     rw = f1["0"]["remote_write"]
     assert "not seen by the owner" in rw and "heap chunk 2 high" in rw and "staging" in rw, f1
     assert f1["2"]["remote_write"] == "ok", f1
+
+
+@pytest.mark.gpu
+def test_preflight_more_than_8_members(tmp_path, monkeypatch):
+    """osgpu_preflight with 10 processes on cuda:0 (more than the team
+    kernel's 8): every probe and remote write of every peer passes, and the
+    bytes next to every written block are untouched (the blocks are sized
+    by the active set)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("OSGPU_HEAP_CHUNK_BYTES", str(64 << 20))
+    world = 10
+    res = launch("preflightwide", world, tmp_path, timeout=300)
+    for r in range(world):
+        x = res[r]
+        assert x["preflight_rc"] == 0 and x["preflight_none_rc"] == 0, x
+        assert sorted(x["preflight"]) == sorted(str(p) for p in range(world) if p != r)
+        for p, e in x["preflight"].items():
+            assert e["chunks"] == 2 and e["status"] == "ok" and e["remote_write"] == "ok", (r, p, e)
+        assert x["guards_intact"], x
 
 
 @pytest.mark.gpu
