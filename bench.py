@@ -253,28 +253,66 @@ def _timer_sig(pet):
                                     ctypes.c_int]
 
 
+def hip_runtime_path():
+    """The libamdhip64 this process has mapped: torch's bundled copy (ROCm
+    7.0 in this image) once torch is imported, /opt/rocm's (7.2) in a
+    process that never imports it."""
+    try:
+        for line in open("/proc/self/maps"):
+            if "libamdhip64" in line:
+                return line.split()[-1]
+    except OSError:
+        pass
+    return None
+
+
 def dma_d2h_state(nbytes=64 << 20, reps=3):
     """The DMA engine's device-to-host rate right now (best of `reps`
     64-MiB copies into pinned memory): 56-57 GB/s when the GPU's power state
-    is up, 28-30 in the low state an idle box starts in (and drops back to
-    at times) -- the state the STAGED path's DMA legs would see
-    (tools/d2h_timeline.hip).  Reported beside the host-staged rates."""
-    import torch
-    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    torch.cuda.synchronize()
+    is up, 28-30 in the low state an idle box starts in (tools/
+    d2h_timeline.hip).  Through the HIP runtime already in the process
+    (ctypes), so it works with or without torch."""
+    hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
+    vp = ctypes.c_void_p
+    d, h = vp(), vp()
+    assert hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipHostMalloc(ctypes.byref(h), ctypes.c_size_t(nbytes), 0) == 0
+    assert hip.hipMemset(d, 1, ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipDeviceSynchronize() == 0
     best = None
     for _ in range(reps):
         t0 = time.perf_counter()
-        h.copy_(d, non_blocking=True)
-        torch.cuda.synchronize()
+        assert hip.hipMemcpy(h, d, ctypes.c_size_t(nbytes), 2) == 0  # D2H
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
-    del d, h
+    hip.hipFree(d)
+    hip.hipHostFree(h)
     return {"dma_d2h_GBs": nbytes / best / 1e9, "low_state": nbytes / best / 1e9 < 40}
 
 
-def host_staged_time(n, reps=5, pes=2):
+def host_staged_child(n, timeout=240):
+    """host_staged_time in a child process that never imports torch, so the
+    library runs on /opt/rocm's HIP runtime as in a C application.  Inside a
+    torch process it runs on torch's bundled ROCm 7.0 runtime, whose D2H
+    copies pick an engine mask of both SDMA engines when both are idle; the
+    copy is refused and redone as a blit kernel ("HSA copy failed with code
+    4097, falling to Blit copy", profiles/r05_torch_runtime_d2h.txt), which
+    caps the duplex pair at 41.9 GB/s each way and, inside the staged
+    pipeline, at 27-35 depending on timing.  The 7.2 runtime picks one
+    engine per direction (48.3 each way)."""
+    import subprocess
+    code = ("import sys, json; sys.path.insert(0, %r); import bench; "
+            "print('RESULT ' + json.dumps(bench.host_staged_time(%d)))") % (ROOT, n)
+    env = dict(os.environ, OSGPU_NO_TORCH="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    if not line:
+        return {"error": (r.stdout + r.stderr)[-600:]}
+    return json.loads(line[0][7:])
+
+
+def host_staged_time(n, reps=7, pes=2, warm_s=1.5):
     """The reference's data placement: sources and targets in HOST symmetric
     heaps.  shmem_double_sum_to_all over a 2-PE set on one GPU (pthreads as
     PEs), STAGED path: H2D own source -> team exchange on the GPU -> D2H,
@@ -291,7 +329,7 @@ def host_staged_time(n, reps=5, pes=2):
                    f"PCIe bytes per call = {P}*{n}*8 H2D + {P}*{n}*8 D2H",
            "stage_copy": os.environ.get("OSGPU_STAGE_COPY", "dma"),
            "copy_streams": os.environ.get("OSGPU_COPY_STREAMS", "prio"),
-           "dma_state": dma_d2h_state()}
+           "dma_state": dma_d2h_state(), "hip_runtime": hip_runtime_path()}
     for pinned in (True, False):
         tm = T.Team(P, 2 * n * 8 + 8192, device=False)
         toff = (n * 8 + 4095) // 4096 * 4096
@@ -305,6 +343,12 @@ def host_staged_time(n, reps=5, pes=2):
         src = (ctypes.c_void_p * P)(*[tm.ptr(pe, 0) for pe in range(P)])
         ps = (ctypes.c_void_p * P)(*[tm.ptr(pe, tm.psync_off) for pe in range(P)])
         _timer_sig(tm.pet)
+        # warm-up: staged calls for warm_s seconds before the timed ones (the
+        # DMA engines' device-to-host rate follows the GPU's power state,
+        # dma_d2h_state; the first calls of a process also map the staging)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < warm_s:
+            tm.pet.pet_time_to_all(fn, P, tgt, src, ps, n, 1)
         sec = tm.pet.pet_time_to_all(fn, P, tgt, src, ps, n, reps)
         want = sum(1.5 + pe for pe in range(P))
         ok = bool((tm.hbuf[tm.hoff + toff: tm.hoff + toff + n * 8].view(np.float64) == want).all())
@@ -317,6 +361,7 @@ def host_staged_time(n, reps=5, pes=2):
             L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
         L.osgpu_finalize()
         del tm
+    out["dma_state_after"] = dma_d2h_state()
     return out
 
 
@@ -845,10 +890,14 @@ def bench_single(args):
                         "completion waits; 4*n*8 HBM bytes per call"}
         except Exception as e:  # report, never hide
             res["api"] = {"error": repr(e)}
-        try:
-            res["host_staged"] = host_staged_time(n)
+        try:  # as a C application runs it: /opt/rocm's HIP runtime, no torch
+            res["host_staged"] = host_staged_child(n)
         except Exception as e:
             res["host_staged"] = {"error": repr(e)}
+        try:  # the same inside this (torch) process: torch's bundled runtime
+            res["host_staged_in_torch_process"] = host_staged_time(n)
+        except Exception as e:
+            res["host_staged_in_torch_process"] = {"error": repr(e)}
         try:
             res["collectives"] = collectives_single()
         except Exception as e:

@@ -97,6 +97,9 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_LDS_U8
 #define OSGPU_TEAM_LDS_U8 4
 #endif
+#ifndef OSGPU_TEAM_LDS_ROT
+#define OSGPU_TEAM_LDS_ROT 0
+#endif
 
 
 // vectors per input per lane for 2 and for 3-4 members (all loaded before
@@ -142,6 +145,21 @@ struct Rounds {
     }
 };
 
+// XCD-aware workgroup -> tile map (OSGPU_TEAM_XCD): the dispatcher deals
+// workgroups round-robin over the 8 XCDs (b % 8), so with the identity map
+// XCD x streams tiles x, x + 8, x + 16, ...; remapped, XCD x streams one
+// contiguous run of tiles.  A bijection on [0, n) for any n.
+#ifndef OSGPU_TEAM_XCD
+#define OSGPU_TEAM_XCD 0
+#endif
+constexpr unsigned kXcds = 8;
+__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned n)
+{
+    if (!OSGPU_TEAM_XCD || n < kXcds) return b;
+    const unsigned x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
+    return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
+
 // E: Elem<T, OP> (exact) or Fast<T, OP> (branch-free, elem_ops.hpp)
 template <typename T, int OP, int P, bool ORDERED, typename E = Elem<T, OP>>
 __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
@@ -182,7 +200,8 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
     // tile blockIdx.x * tm + tk (launch_team_tiles; tm = 1, tk = 0: tile blockIdx.x)
-    const size_t t0 = ((size_t) blockIdx.x * tm + tk) * (kTeamBlock * U) + threadIdx.x;
+    const size_t t0 = ((size_t) xcd_tile(blockIdx.x, gridDim.x) * tm + tk) * (kTeamBlock * U) +
+                      threadIdx.x;
     // fold one vector of every input into one vector of every output: the
     // branch-free fold first, the exact one only for a vector whose results
     // hold a NaN part (rare; elem_ops.hpp Fast) -- no branch per element, so
@@ -339,7 +358,15 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
 #pragma unroll
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
-    const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
+    const int wave = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
+    // the member this wave stages and writes: wave w, or with
+    // OSGPU_TEAM_LDS_ROT member (w + blockIdx.x) % P (the waves of
+    // neighbouring workgroups start on different arrays)
+#if OSGPU_TEAM_LDS_ROT
+    const int w = __builtin_amdgcn_readfirstlane((int) ((wave + blockIdx.x) % P));
+#else
+    const int w = wave;
+#endif
     const int lane = (int) (threadIdx.x & 63);
     const u32x4 *src = reinterpret_cast<const u32x4 *>(pick(a.src, w) + head);
     u32x4 *dst = reinterpret_cast<u32x4 *>(pick(a.dst, w) + head);
@@ -392,7 +419,7 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
             }
         });
     };
-    const size_t t = (size_t) blockIdx.x * tm + tk;
+    const size_t t = (size_t) xcd_tile(blockIdx.x, gridDim.x) * tm + tk;
     load(t);
 #pragma unroll
     for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];

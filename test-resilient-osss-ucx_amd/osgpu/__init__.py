@@ -86,11 +86,14 @@ def load() -> ctypes.CDLL:
     # SONAME libamdhip64.so.7, different file name).  Loaded first, our
     # NEEDED entry binds to torch's copy; loaded after us, torch would map a
     # second runtime next to /opt/rocm's and the two corrupt each other's
-    # heap at exit.  So when torch is importable, it goes first.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # heap at exit.  So when torch is importable, it goes first -- unless
+    # OSGPU_NO_TORCH=1: a process that never imports torch (as a C
+    # application linking the library) runs on /opt/rocm's runtime.
+    if os.environ.get("OSGPU_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     for name in ENTRY_POINTS:

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Build libosgpu_reduce variants into tools/ab/<name>/ for one-lease A/B runs
+# (tools/ab is gpurun-ignored by default: the calling script lists it).
+#   tools/build_ab.sh name "-DFLAG=1 -DOTHER=2" [name2 "flags2" ...]
+set -e
+cd "$(dirname "$0")/../test-resilient-osss-ucx_amd/csrc"
+make -s -j8
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math"
+while [ $# -ge 2 ]; do
+  name=$1; X=$2; shift 2
+  d=../../tools/ab/$name; mkdir -p $d
+  /opt/rocm/bin/hipcc $FL $X -c combine.hip -o $d/combine.o &
+  /opt/rocm/bin/hipcc $FL $X -c team.hip -o $d/team.o &
+  /opt/rocm/bin/hipcc $FL $X -c fused.hip -o $d/fused.o &
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
+      $d/combine.o $d/team.o $d/fused.o verify.o longdouble.o copy.o runtime.o heap.o \
+      shmem_reduce.o shmem_collect.o -lrccl -ldl -lpthread
+  rm -f $d/*.o
+  echo "built tools/ab/$name"
+done

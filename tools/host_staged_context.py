@@ -20,6 +20,10 @@ STEPS = {
     "torch_alloc": "x = torch.empty(3 << 30, dtype=torch.uint8, device='cuda'); x.fill_(1); "
                    "del x; torch.cuda.empty_cache()",
     "api": "bench.api_call_time(N)",
+    "placements": "L = osgpu.load()\nfor P in (2, 4, 8): bench.team_placements(L, torch, N, 5, P)",
+    "headline": "L = osgpu.load(); bench.kernel_rate(L, torch, 5, 0, N, 8, torch.float64, "
+                "lambda x, k: x.uniform_(1.0, 2.0))",
+    "extra": "L = osgpu.load(); bench.extra_kernel_rates(L, torch)",
     "side_stream": "s = torch.cuda.Stream(); x = torch.ones(1 << 20, device='cuda')\n"
                    "with torch.cuda.stream(s): x.add_(1)\ntorch.cuda.synchronize()",
     "events": "e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)\n"
@@ -48,6 +52,9 @@ def run(prefix):
     code.append("print('RESULT ' + json.dumps(bench.host_staged_time(N)))")
     r = subprocess.run([sys.executable, "-c", "\n".join(code)], capture_output=True, text=True,
                        timeout=300, cwd=ROOT, env=dict(os.environ, **ENV))
+    if os.environ.get("CTX_STDERR"):  # keep the child's stderr (HIP logs)
+        with open(os.environ["CTX_STDERR"] + "." + "+".join(prefix), "w") as f:
+            f.write(r.stderr)
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
     out = json.loads(line[0][7:]) if line else {"error": r.stderr[-800:]}
     out.pop("note", None)

@@ -106,8 +106,25 @@ int main(int argc, char **argv)
             }
             CK(hipDeviceSynchronize());
             hipStream_t si, so;
-            CK(hipStreamCreateWithFlags(&si, hipStreamNonBlocking));
-            CK(hipStreamCreateWithFlags(&so, hipStreamNonBlocking));
+            // argv[5]: copy streams 0 default priority, 1 in lowest / out
+            // highest, 2 in highest / out lowest, 3 both lowest, 4 both
+            // highest, 5 both CU-masked (a queue each)
+            const int smode = argc > 5 ? atoi(argv[5]) : 0;
+            int lo = 0, hi = 0;
+            CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            auto mk = [&](hipStream_t *s, int pr) {
+                if (smode == 0) {
+                    CK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+                } else if (smode == 5) {
+                    uint32_t m[8];
+                    for (auto &w : m) w = 0xffffffffu;
+                    CK(hipExtStreamCreateWithCUMask(s, 8, m));
+                } else {
+                    CK(hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr));
+                }
+            };
+            mk(&si, smode == 1 || smode == 3 ? lo : hi);
+            mk(&so, smode == 2 || smode == 3 ? lo : hi);
             double best[3] = {1e9, 1e9, 1e9};  // h2d alone, d2h alone, both
             for (int r = 0; r < reps; r++) {
                 double t0 = now();
@@ -127,9 +144,9 @@ int main(int argc, char **argv)
                 best[1] = std::min(best[1], t2 - t1);
                 best[2] = std::min(best[2], t3 - t2);
             }
-            printf("{\"gpu_bus\": \"%s\", \"gpu_node\": %d, \"bind\": %d, \"cpu\": %d, \"in_node\": %d, \"out_node\": %d, \"before\": %d, \"pre_streams\": %d, \"pre_used\": %d, \"bytes\": %zu, \"h2d_GBs\": %.2f, "
+            printf("{\"smode\": %d, \"gpu_bus\": \"%s\", \"gpu_node\": %d, \"bind\": %d, \"cpu\": %d, \"in_node\": %d, \"out_node\": %d, \"before\": %d, \"pre_streams\": %d, \"pre_used\": %d, \"bytes\": %zu, \"h2d_GBs\": %.2f, "
                    "\"d2h_GBs\": %.2f, \"duplex_GBs_each_way\": %.2f}\n",
-                   bus, gpu_node, node, sched_getcpu(), page_node(h_in), page_node(h_out), before, k, used, nb, nb / best[0] / 1e9, nb / best[1] / 1e9, nb / best[2] / 1e9);
+                   smode, bus, gpu_node, node, sched_getcpu(), page_node(h_in), page_node(h_out), before, k, used, nb, nb / best[0] / 1e9, nb / best[1] / 1e9, nb / best[2] / 1e9);
             fflush(stdout);
             CK(hipStreamDestroy(si));
             CK(hipStreamDestroy(so));
