@@ -378,6 +378,13 @@ def collectives_single(P=4, nb=64 << 20, reps=10):
     t = CB.api_time("fcollect", P, nb, reps, True)
     out["fcollect64_device"] = {"pes": P, "bytes_per_pe": nb, "ms_per_call": t * 1e3,
                                 "GBps_all_pes": CB.moved("fcollect", P, nb) / t / 1e9}
+    # host symmetric heaps (pageable): the STAGED path, H2D / exchange / D2H
+    # pipelined over two slots; the P PEs share this GPU's PCIe link
+    nh = nb // 4
+    t = CB.api_time("fcollect", P, nh, 5, False)
+    out["fcollect64_host_staged"] = {
+        "pes": P, "bytes_per_pe": nh, "ms_per_call": t * 1e3,
+        "pcie_h2d_GBs": P * nh / t / 1e9, "pcie_d2h_GBs": P * P * nh / t / 1e9}
     return out
 
 

@@ -145,10 +145,14 @@ struct Rounds {
     }
 };
 
-// XCD-aware workgroup -> tile map (OSGPU_TEAM_XCD): the dispatcher deals
-// workgroups round-robin over the 8 XCDs (b % 8), so with the identity map
-// XCD x streams tiles x, x + 8, x + 16, ...; remapped, XCD x streams one
-// contiguous run of tiles.  A bijection on [0, n) for any n.
+// XCD-aware workgroup -> tile map (OSGPU_TEAM_XCD, off): the dispatcher
+// deals workgroups round-robin over the 8 XCDs (b % 8), so with the identity
+// map XCD x streams tiles x, x + 8, x + 16, ...; remapped, XCD x streams one
+// contiguous run of tiles.  A bijection on [0, n) for any n.  Measured
+// slower at every member count over ten array layouts (of the same-mix
+// copy: 2 members 0.954 vs 0.978 median, 4 members 0.934 vs 0.962, 8
+// members 0.853 vs 0.886; tools/team_layout_sweep.py,
+// profiles/r05_team_layouts.jsonl), so the identity map ships.
 #ifndef OSGPU_TEAM_XCD
 #define OSGPU_TEAM_XCD 0
 #endif
