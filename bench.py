@@ -454,7 +454,7 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
     return span_per_launch(torch, st, launch, reps), a, b, out
 
 
-def team_kernel_rate(L, torch, n, reps, P=2):
+def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
     registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>,
     team_lds_kernel<double,SUM,P> at 3 and 4 members
@@ -465,12 +465,30 @@ def team_kernel_rate(L, torch, n, reps, P=2):
     the launch stream.  Beside it the same-mix ceiling: the copy kernel
     (csrc/copy.hip) moving P ranges of n*8 bytes in one launch, its tiles
     dealt round-robin over the ranges -- P read and P write streams at once
-    over the same bytes, nothing folded."""
+    over the same bytes, nothing folded.
+    layout "alloc": every array its own allocation; "symheap": P symmetric
+    heaps carved back to back out of ONE allocation (as PE threads' heaps in
+    one buffer), member p's source at offset 0 of heap p and its target at
+    n*8 + 2 MiB: every array shares its low 21 address bits and the regular
+    high bits of one allocation -- the worst layout the sweep found
+    (tools/team_layout_sweep.py symheap, profiles/r05_team_symheap.jsonl);
+    heaps from osgpu_heap_create (one allocation each) do not show it
+    (profiles/r05_heap_stagger_ab.jsonl)."""
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(11 + P)
-    srcs_t = [torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0, generator=g)
-              for _ in range(P)]
-    dsts_t = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(P)]
+    if layout == "symheap":
+        heap = (2 * n * 8 + (4 << 20) + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+        buf = torch.empty(P * heap + (2 << 20), dtype=torch.uint8, device=dev)
+        b0 = (-buf.data_ptr()) % (2 << 20)
+        srcs_t = [buf[b0 + p * heap: b0 + p * heap + n * 8].view(torch.float64) for p in range(P)]
+        dsts_t = [buf[b0 + p * heap + n * 8 + (2 << 20): b0 + p * heap + 2 * n * 8 + (2 << 20)]
+                  .view(torch.float64) for p in range(P)]
+        for x in srcs_t:
+            x.uniform_(1.0, 2.0, generator=g)
+    else:
+        srcs_t = [torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0, generator=g)
+                  for _ in range(P)]
+        dsts_t = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(P)]
     st = torch.cuda.Stream(device=dev)
     srcs = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs_t])
     dsts = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts_t])
@@ -525,7 +543,7 @@ def team_kernel_rate(L, torch, n, reps, P=2):
            "traffic_source": tr.get("source") if tr else None,
            "kernel": ("osgpu::" + kern.replace("<double, 0,", "<double, SUM,") +
                       (">" if lds else "")),
-           "members": P, "nreduce": n,
+           "members": P, "nreduce": n, "layout": layout,
            "kernel_avg_us": kavg * 1e6,
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
            "kernel_min_us_per_launch_events": min(ks) * 1e6,
@@ -534,9 +552,16 @@ def team_kernel_rate(L, torch, n, reps, P=2):
                                      "ranges": P, "bytes_per_range": n * 8, "us": cavg * 1e6,
                                      "frac_of_8TBs": cfrac},
            "frac_of_copy_ceiling": frac / cfrac,
+           # where the arrays landed (virtual; each a separate allocation):
+           # base addresses and their offsets within a 2 MiB fragment
+           "addresses": {"src": [hex(x.data_ptr()) for x in srcs_t],
+                         "dst": [hex(x.data_ptr()) for x in dsts_t],
+                         "offset_in_2MiB": [x.data_ptr() % (2 << 20) for x in srcs_t + dsts_t]},
            "note": f"one launch over all nreduce elements = the {P} PEs' shard launches of a "
                    f"{P}-PE call; {P} reads + {P} writes of 8 B per element"}
     del srcs_t, dsts_t
+    if layout == "symheap":
+        del buf
     torch.cuda.empty_cache()
     return out
 
@@ -552,11 +577,26 @@ def team_placements(L, torch, n, reps, P, trials=3):
     runs = [team_kernel_rate(L, torch, n, reps, P) for _ in range(trials)]
     med = sorted(runs, key=lambda r: r["frac_of_copy_ceiling"])[len(runs) // 2]
     out = dict(med)
+    # heaps carved out of one allocation (equal low address bits, regular
+    # high ones): the worst layout measured, reported beside the placements
+    try:
+        sh = team_kernel_rate(L, torch, n, reps, P, layout="symheap")
+        out["one_allocation_heaps_layout"] = {
+            "frac": sh["frac"], "copy_frac": sh["copy_ceiling_same_mix"]["frac_of_8TBs"],
+            "frac_of_copy_ceiling": sh["frac_of_copy_ceiling"],
+            "kernel_avg_us": sh["kernel_avg_us"], "bit_exact_sample": sh["bit_exact_sample"],
+            "offset_in_2MiB": sh["addresses"]["offset_in_2MiB"]}
+    except Exception as e:  # report, never hide
+        out["one_allocation_heaps_layout"] = {"error": repr(e)[:200]}
     out["placements"] = [{"frac": r["frac"], "copy_frac": r["copy_ceiling_same_mix"]["frac_of_8TBs"],
                           "frac_of_copy_ceiling": r["frac_of_copy_ceiling"],
                           "kernel_avg_us": r["kernel_avg_us"]} for r in runs]
+    for key, get in (("frac", lambda r: r["frac"]),
+                     ("frac_of_copy_ceiling", lambda r: r["frac_of_copy_ceiling"])):
+        v = sorted(get(r) for r in runs)
+        out[key + "_min"], out[key + "_median"], out[key + "_max"] = v[0], v[len(v) // 2], v[-1]
     out["placements_note"] = (f"{trials} allocations; the fields above are the trial with the "
-                              f"median frac_of_copy_ceiling")
+                              f"median frac_of_copy_ceiling, *_min / *_median / *_max over all")
     out["bit_exact_sample"] = all(r["bit_exact_sample"] for r in runs)
     return out
 

@@ -437,19 +437,16 @@ void run_rccl(const CCall &c)
 // ------------------------------------------------------------ STAGED (host)
 
 // Chunk k covers source bytes [k*C, (k+1)*C) of every member.  Each PE
-// stages its chunk in an `in` slot of its device staging; each PE's copy
+// stages its chunk in the `in` area of its device staging; each PE's copy
 // kernel pulls the parts of its pieces inside chunk k from the members' `in`
-// slots (IPC-mapped) into its own `out` slot; D2H to the target.  Two slots
-// of each, used by alternate chunks, so the H2D of chunk k+1 and the D2H of
-// chunk k-1 run while chunk k is exchanged (the reduce's pipeline,
-// shmem_reduce.cpp run_staged).  The four slots of a StageSet are one
-// region per member: [in 0 | in 1 | out 0 | out 1], C and P*C bytes.
+// areas (IPC-mapped) into its own `out` area; D2H to the target.  The four
+// slots of a StageSet are one region: in = C bytes, out = P*C bytes.
 void run_staged(const CCall &c, StageSet &S)
 {
     t_last_coll = OSGPU_RAN_STAGED;
     const int P = c.PE_size;
     const size_t region = 4 * S.slot;
-    size_t C = region / (2 * (size_t) (P + 1));
+    size_t C = region / (size_t) (P + 1);
     C &= ~(size_t) 255;
     if (C == 0) fatal(c.name, "staging too small for %d PEs", P);
     size_t maxlen = 0;
@@ -459,36 +456,28 @@ void run_staged(const CCall &c, StageSet &S)
     const bool tmp = overlap2(c.target, c.out_bytes, c.source, mine);
     char *result = tmp ? (char *) malloc(c.out_bytes) : (char *) c.target;
     if (tmp && !result) fatal(c.name, "out of memory for the temporary target");
-    auto in_of = [&](int member, size_t k) { return S.region(member) + (k & 1) * C; };
-    auto out_me = [&](size_t k) { return S.region(c.idx) + 2 * C + (k & 1) * (size_t) P * C; };
+    char *in_me = S.region(c.idx);
+    char *out_me = S.region(c.idx) + C;
     std::vector<osgpu::CopySeg> segs;
     std::vector<size_t> seg_dst;  // target offset of each staged piece part
-    // my chunk k's H2D (slot k & 1 is free: its readers, chunk k - 2's copy
-    // kernels, finished before the barrier that ended iteration k - 2)
-    auto h2d = [&](size_t k) {
-        const size_t lo = k * C;
-        if (mine > lo)
-            HIPCHK(c.name, hipMemcpyAsync(in_of(c.idx, k), (const char *) c.source + lo,
-                                          std::min(mine, lo + C) - lo, hipMemcpyHostToDevice,
-                                          S.st_in));
-        HIPCHK(c.name, hipEventRecord(S.ev_in[k & 1], S.st_in));
-    };
 
     entry_sync(c.name);
-    if (nchunks) h2d(0);
     for (size_t k = 0; k < nchunks; k++) {
         const size_t lo = k * C, hi = lo + C;
-        if (k + 1 < nchunks) h2d(k + 1);
-        HIPCHK(c.name, hipEventSynchronize(S.ev_in[k & 1]));
-        if (k >= 2) HIPCHK(c.name, hipEventSynchronize(S.ev_out[k & 1]));  // out slot drained
-        barrier(c);  // chunk k staged everywhere; every `in` slot of k - 2 drained
+        if (mine > lo) {
+            const size_t n = std::min(mine, hi) - lo;
+            HIPCHK(c.name, hipMemcpyAsync(in_me, (const char *) c.source + lo, n,
+                                          hipMemcpyHostToDevice, S.st_in));
+            stream_wait(c.name, S.st_in);
+        }
+        barrier(c);  // chunk k staged everywhere; every `in` area of k-1 drained
         segs.clear();
         seg_dst.clear();
         size_t packed = 0;
         for (const Piece &p : c.pieces) {
             const size_t a = std::max(p.src_off, lo), b = std::min(p.src_off + p.len, hi);
             if (a >= b) continue;
-            segs.push_back({in_of(p.from, k) + (a - lo), out_me(k) + packed, b - a});
+            segs.push_back({S.region(p.from) + (a - lo), out_me + packed, b - a});
             seg_dst.push_back(p.dst_off + (a - p.src_off));
             packed += b - a;
         }
@@ -498,9 +487,8 @@ void run_staged(const CCall &c, StageSet &S)
         for (size_t i = 0; i < segs.size(); i++)
             HIPCHK(c.name, hipMemcpyAsync(result + seg_dst[i], segs[i].dst, segs[i].bytes,
                                           hipMemcpyDeviceToHost, S.st_out));
-        HIPCHK(c.name, hipEventRecord(S.ev_out[k & 1], S.st_out));
+        stream_wait(c.name, S.st_out);
     }
-    stream_wait(c.name, S.st_out);
     if (tmp) {
         memcpy(c.target, result, c.out_bytes);
         free(result);

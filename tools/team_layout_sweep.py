@@ -47,6 +47,10 @@ def families(P):
     for r in range(3):
         offs = [rnd.randrange(0, 512) * 4 * KiB for _ in range(2 * P)]
         fam[f"rand4K_{r}"] = (lambda o: (lambda i: o[i]))(offs)
+    for k in ("symheap", "symheap+4K", "symheap+64K", "symheap+1M"):
+        fam[k] = None
+    if os.environ.get("SWEEP_ONLY"):
+        fam = {k: v for k, v in fam.items() if k in os.environ["SWEEP_ONLY"].split(",")}
     return fam
 
 
@@ -56,7 +60,7 @@ def main():
     st = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(st.cuda_stream)
     P_max = max(MEMBERS)
-    slack = 2 * P_max * (4 * MiB + 4 * MiB) + 32 * MiB
+    slack = 2 * P_max * (4 * MiB + 4 * MiB) + P_max * MiB + 32 * MiB
     buf = torch.empty(2 * P_max * N * 8 + slack, dtype=torch.uint8, device=dev)
     base = (buf.data_ptr() + 2 * MiB - 1) // (2 * MiB) * (2 * MiB)
     torch.cuda.synchronize()
@@ -75,8 +79,17 @@ def main():
 
     for P in MEMBERS:
         for name, skew in families(P).items():
-            # array i; the 4 MiB spacing beyond n*8 keeps skewed arrays apart
-            addr = [base + i * (N * 8 + 4 * MiB) + skew(i) for i in range(2 * P)]
+            if name.startswith("symheap"):
+                # a symmetric heap per member: source at 0, target at n*8 +
+                # 2 MiB of heap p; heaps back to back (+ an optional skew per heap)
+                H = 2 * N * 8 + 4 * MiB
+                d = {"symheap": 0, "symheap+4K": 4 * KiB, "symheap+64K": 64 * KiB,
+                     "symheap+1M": MiB}[name]
+                addr = [base + p * (H + d) for p in range(P)] + \
+                       [base + p * (H + d) + N * 8 + 2 * MiB for p in range(P)]
+            else:
+                # array i; the 4 MiB spacing beyond n*8 keeps skewed arrays apart
+                addr = [base + i * (N * 8 + 4 * MiB) + skew(i) for i in range(2 * P)]
             assert addr[-1] + N * 8 <= buf.data_ptr() + buf.numel()
             for i in range(P):  # sources: a known value per member
                 tmp = torch.full((N,), 1.0 + i / 8, dtype=torch.float64, device=dev)
