@@ -105,3 +105,49 @@ def test_config5_float_128Mi_8_pes(torch_cuda, op, lo, hi):
         del want
     del srcs, dsts
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_config5_host_staged_128Mi_8_pes(torch_cuda, pinned):
+    """BASELINE config 5 as the reference places it: sources and targets in
+    HOST symmetric heaps (8 PE threads, 128 Mi floats per PE), the STAGED
+    path (H2D of each PE's source, the team exchange on the GPU, D2H) for
+    float min, max and prod in turn, on a heap pinned with
+    osgpu_host_register and on a pageable one (the library's bounce).  Every
+    member's target is checked bit for bit against its own fold order
+    (_fold, on the GPU)."""
+    import numpy as np
+    torch = torch_cuda
+    from support import team as T
+    n = 128 << 20
+    nb = n * 4
+    _need(torch, (3 * P + 2) * nb)
+    L = osgpu.load()
+    L.osgpu_finalize()
+    tm = T.Team(P, 2 * nb + 8192, device=False)
+    toff = T._align(nb)
+    if pinned:
+        assert L.osgpu_host_register(ctypes.c_void_p(tm.base), P * tm.H) == 0
+    try:
+        for op, lo, hi in (("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1)):
+            g = torch.Generator(device="cuda:0").manual_seed(55)
+            srcs = [torch.empty(n, dtype=torch.float32, device="cuda:0").uniform_(
+                lo, hi, generator=g) for _ in range(P)]
+            for pe in range(P):
+                a = tm.hoff + pe * tm.H
+                torch.from_numpy(tm.hbuf[a:a + nb].view(np.float32)).copy_(srcs[pe])
+            tm.run("float", op, toff, 0, n)
+            assert set(tm.last_paths.values()) == {"staged"}, tm.last_paths
+            for q in range(P):
+                a = tm.hoff + q * tm.H + toff
+                got = torch.from_numpy(tm.hbuf[a:a + nb].view(np.int32)).to("cuda:0")
+                want = _fold(torch, op, srcs, q)
+                assert torch.equal(got, want.view(torch.int32)), (op, q)
+                del got, want
+            del srcs
+    finally:
+        if pinned:
+            L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
+        L.osgpu_finalize()
+        del tm
+        torch.cuda.empty_cache()
