@@ -290,7 +290,65 @@ def dma_d2h_state(nbytes=64 << 20, reps=3):
     return {"dma_d2h_GBs": nbytes / best / 1e9, "low_state": nbytes / best / 1e9 < 40}
 
 
-def host_staged_child(n, timeout=240):
+def host_staged_config5(n=128 << 20, P=8, reps=3, warm_s=1.5):
+    """BASELINE config 5 with its H2D/D2H copies: shmem_float_{min,max,prod}
+    _to_all over 8 PEs (pthreads) on one GPU, 128 Mi floats per PE in a HOST
+    symmetric heap pinned with osgpu_host_register -- the STAGED path (H2D of
+    each PE's source, the team exchange on the GPU, D2H of its target).  All
+    8 PEs share this GPU's PCIe link: 8 * n * 4 bytes each way per call.
+    Timed in C after a warm-up; every member's target sampled against its
+    own fold order (numpy, src/reductions.c:79-111)."""
+    import numpy as np
+    import osgpu
+    from support import team as T
+    L = osgpu.load()
+    L.osgpu_finalize()
+    nb = n * 4
+    tm = T.Team(P, 2 * nb + 8192, device=False)
+    toff = T._align(nb)
+    rng = np.random.default_rng(5)
+    out = {"pes": P, "nreduce": n, "bytes_per_pe": nb, "heap": "pinned host (osgpu_host_register)",
+           "pcie_bytes_each_way_per_call": P * nb, "hip_runtime": hip_runtime_path()}
+    assert L.osgpu_host_register(ctypes.c_void_p(tm.base), P * tm.H) == 0
+    try:
+        for op, lo, hi in (("min", -1e3, 1e3), ("max", -1e3, 1e3), ("prod", 0.9, 1.1)):
+            for pe in range(P):  # a 1 Mi random block per PE, tiled
+                blk = rng.uniform(lo, hi, 1 << 20).astype(np.float32)
+                a = tm.hoff + pe * tm.H
+                tm.hbuf[a:a + nb].view(np.float32).reshape(-1, 1 << 20)[:] = blk
+            fn = ctypes.cast(getattr(L, f"shmem_float_{op}_to_all"), ctypes.c_void_p)
+            tgt = (ctypes.c_void_p * P)(*[tm.ptr(pe, toff) for pe in range(P)])
+            src = (ctypes.c_void_p * P)(*[tm.ptr(pe, 0) for pe in range(P)])
+            ps = (ctypes.c_void_p * P)(*[tm.ptr(pe, tm.psync_off) for pe in range(P)])
+            _timer_sig(tm.pet)
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < warm_s:
+                tm.pet.pet_time_to_all(fn, P, tgt, src, ps, n, 1)
+            sec = tm.pet.pet_time_to_all(fn, P, tgt, src, ps, n, reps)
+            idx = rng.integers(0, n, 1 << 16)
+            xs = [tm.hbuf[tm.hoff + pe * tm.H:][:nb].view(np.float32)[idx] for pe in range(P)]
+            f = {"min": lambda a, b: np.where(a < b, a, b),
+                 "max": lambda a, b: np.where(a > b, a, b),
+                 "prod": lambda a, b: (a * b).astype(np.float32)}[op]
+            ok = True
+            for q in range(P):
+                acc = xs[q].copy()
+                for j in range(P):
+                    if j != q:
+                        acc = f(acc, xs[j])
+                got = tm.hbuf[tm.hoff + q * tm.H + toff:][:nb].view(np.float32)[idx]
+                ok = ok and bool(np.array_equal(got.view(np.int32), acc.view(np.int32)))
+            out[op] = {"ms_per_call": sec * 1e3, "pcie_GBs_each_way": P * nb / sec / 1e9,
+                       "correct_sample": ok}
+    finally:
+        L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
+        L.osgpu_finalize()
+        del tm
+    out["dma_state_after"] = dma_d2h_state()
+    return out
+
+
+def host_staged_child(n, timeout=240, what="host_staged_time(%d)"):
     """host_staged_time in a child process that never imports torch, so the
     library runs on /opt/rocm's HIP runtime as in a C application.  Inside a
     torch process it runs on torch's bundled ROCm 7.0 runtime, whose D2H
@@ -302,7 +360,7 @@ def host_staged_child(n, timeout=240):
     engine per direction (48.3 each way)."""
     import subprocess
     code = ("import sys, json; sys.path.insert(0, %r); import bench; "
-            "print('RESULT ' + json.dumps(bench.host_staged_time(%d)))") % (ROOT, n)
+            "print('RESULT ' + json.dumps(bench." + what + "))") % (ROOT, n)
     env = dict(os.environ, OSGPU_NO_TORCH="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=timeout, cwd=ROOT)
@@ -941,6 +999,10 @@ def bench_single(args):
             res["host_staged"] = host_staged_child(n)
         except Exception as e:
             res["host_staged"] = {"error": repr(e)}
+        try:  # config 5 with its H2D/D2H copies, the same child process
+            res["config5_host_staged"] = host_staged_child(128 << 20, what="host_staged_config5(%d)")
+        except Exception as e:
+            res["config5_host_staged"] = {"error": repr(e)}
         try:  # the same inside this (torch) process: torch's bundled runtime
             res["host_staged_in_torch_process"] = host_staged_time(n)
         except Exception as e:
