@@ -209,8 +209,11 @@ struct LdTeam {
 // At least 4 waves per SIMD (<= 128 VGPRs): the 8-member sum's rounds want
 // 132, and 3 waves per SIMD cost the same-sign sums 6-7 % (interleaved A/B,
 // profiles/r03_ld_variants.jsonl).
+#ifndef OSGPU_LD_WAVES
+#define OSGPU_LD_WAVES 4
+#endif
 template <int OP, int P, bool VEC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ld_team_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OSGPU_LD_WAVES))) void ld_team_kernel(
     LdTeam a, size_t n)
 {
     const size_t stride = (size_t) gridDim.x * blockDim.x;

@@ -12,9 +12,10 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc $FL $X -c combine.hip -o $d/combine.o &
   /opt/rocm/bin/hipcc $FL $X -c team.hip -o $d/team.o &
   /opt/rocm/bin/hipcc $FL $X -c fused.hip -o $d/fused.o &
+  /opt/rocm/bin/hipcc $FL $X -c longdouble.hip -o $d/longdouble.o &
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
-      $d/combine.o $d/team.o $d/fused.o verify.o longdouble.o copy.o runtime.o heap.o \
+      $d/combine.o $d/team.o $d/fused.o verify.o $d/longdouble.o copy.o runtime.o heap.o \
       shmem_reduce.o shmem_collect.o -lrccl -ldl -lpthread
   rm -f $d/*.o
   echo "built tools/ab/$name"
