@@ -43,6 +43,9 @@ import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# team.hip OSGPU_TEAM_LDS_U: vectors per lane per tile of the LDS-staged team
+# kernel at 3-4 members (its template argument, the rocprof name's last field)
+TEAM_LDS_U = 2
 for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
@@ -125,7 +128,7 @@ def live_traffic(n, members=(2, 4, 8), reps=5, timeout=120):
         return {"_error": "rocprofv3 not on PATH"}
     keys = {"combine_vec_kernel<double, 0, 2>": 24}
     for P in members:
-        keys[(f"team_lds_kernel<double, 0, {P}, true, 4" if 3 <= P <= 4
+        keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if 3 <= P <= 4
               else f"team_vec_kernel<double, 0, {P}, true>")] = 16 * P
     tmp = tempfile.mkdtemp(prefix="osgpu_pmc_")
     dirs = {}
@@ -589,9 +592,9 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     cavg = span_per_launch(torch, st, copy, reps)
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
-    # kernel (U = 4) at 3 and 4 members, the register kernel otherwise
+    # kernel (U = TEAM_LDS_U) at 3 and 4 members, the register kernel otherwise
     lds = 3 <= P <= 4
-    kern = (f"team_lds_kernel<double, 0, {P}, true, 4" if lds    # (PMC files' key)
+    kern = (f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if lds    # (PMC files' key)
             else f"team_vec_kernel<double, 0, {P}, true>")
     tr = load_traffic(kern, n)
     frac = B / kavg / 1e9 / HBM_PEAK_GBS

@@ -73,10 +73,15 @@ constexpr int kTeamBlock = 256;
 #define OSGPU_TEAM_PEROUT 1
 #endif
 // from this many members on: the LDS-staged kernel (team_lds_kernel), one
-// wave per member, OSGPU_TEAM_LDS_U 16-B vectors per lane per tile (U = 4:
-// 1.01-1.02 of the copy against 0.95-0.97 for U = 2 at 3-7 members,
-// profiles/r04_team_sweep_3.jsonl; U = 8, 64 KiB of LDS per workgroup at 8
-// members, 0.44-0.62, r04_team_sweep_2.jsonl)
+// wave per member, OSGPU_TEAM_LDS_U 16-B vectors per lane per tile.  U = 2
+// (2 KiB per member per workgroup): timed against U = 4 in one process on
+// the same fresh allocations (tools/team_inproc_ab.py, 10 allocations per
+// member count on each of two leases, profiles/r05_team_p34_ab.jsonl) it ran
+// 1.02-1.04x faster on average at 3 and 4 members and lifted the slowest
+// placement most (4 members: 0.749 against 0.683 of 8 TB/s), losing up to
+// 4 % only where the copy itself was fastest.  (Round 4 had chosen U = 4
+// from a sweep on one box: r04_team_sweep_3.jsonl.)  U = 8, 64 KiB of LDS
+// per workgroup at 8 members: 0.44-0.62, r04_team_sweep_2.jsonl
 #ifndef OSGPU_TEAM_LDS_MIN_P
 #define OSGPU_TEAM_LDS_MIN_P 3
 #endif
@@ -92,7 +97,7 @@ constexpr int kTeamBlock = 256;
 #define OSGPU_TEAM_LDS_MAX_P 4
 #endif
 #ifndef OSGPU_TEAM_LDS_U
-#define OSGPU_TEAM_LDS_U 4
+#define OSGPU_TEAM_LDS_U 2
 #endif
 #ifndef OSGPU_TEAM_LDS_U8
 #define OSGPU_TEAM_LDS_U8 4

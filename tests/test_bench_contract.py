@@ -115,3 +115,14 @@ def test_defaults_single_gpu_within_minutes():
     finally:
         sys.argv = old
     assert a.gpus == 1 and a.nreduce == 64 << 20 and 0 < a.steps <= 100 and 0 <= a.warmup
+
+
+def test_bench_names_the_shipped_lds_tile():
+    """bench.py looks the LDS team kernel up by its rocprof name, whose last
+    template argument is team.hip's OSGPU_TEAM_LDS_U: the two must agree."""
+    import re
+    sys.path.insert(0, ROOT)
+    import bench
+    src = open(os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc", "team.hip")).read()
+    m = re.search(r"#ifndef OSGPU_TEAM_LDS_U\s*\n#define OSGPU_TEAM_LDS_U (\d+)", src)
+    assert m and int(m.group(1)) == bench.TEAM_LDS_U
