@@ -590,6 +590,9 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     for _ in range(3):
         copy()
     cavg = span_per_launch(torch, st, copy, reps)
+    # the team kernel again on the same arrays after the copy: a slow first
+    # timing that is fast here was a transient of the box, not the placement
+    kavg_again = span_per_launch(torch, st, launch, reps)
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
     # kernel (U = TEAM_LDS_U) at 3 and 4 members, the register kernel otherwise
@@ -608,6 +611,7 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
            "kernel_avg_us": kavg * 1e6,
            "kernel_avg_how": "HIP event span over the launches, back to back, / launches",
            "kernel_min_us_per_launch_events": min(ks) * 1e6,
+           "kernel_avg_us_again_after_copy": kavg_again * 1e6,
            "algorithmic_bytes_per_launch": B, "launches": reps, "bit_exact_sample": exact,
            "copy_ceiling_same_mix": {"kernel": "copy_vec_kernel (ranges dealt round-robin)",
                                      "ranges": P, "bytes_per_range": n * 8, "us": cavg * 1e6,
@@ -651,7 +655,10 @@ def team_placements(L, torch, n, reps, P, trials=3):
         out["one_allocation_heaps_layout"] = {"error": repr(e)[:200]}
     out["placements"] = [{"frac": r["frac"], "copy_frac": r["copy_ceiling_same_mix"]["frac_of_8TBs"],
                           "frac_of_copy_ceiling": r["frac_of_copy_ceiling"],
-                          "kernel_avg_us": r["kernel_avg_us"]} for r in runs]
+                          "kernel_avg_us": r["kernel_avg_us"],
+                          "kernel_avg_us_again_after_copy": r["kernel_avg_us_again_after_copy"],
+                          "src": r["addresses"]["src"], "dst": r["addresses"]["dst"]}
+                         for r in runs]
     for key, get in (("frac", lambda r: r["frac"]),
                      ("frac_of_copy_ceiling", lambda r: r["frac_of_copy_ceiling"])):
         v = sorted(get(r) for r in runs)
