@@ -44,8 +44,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # team.hip OSGPU_TEAM_LDS_U: vectors per lane per tile of the LDS-staged team
-# kernel at 3-4 members (its template argument, the rocprof name's last field)
+# kernel (its template argument, the rocprof name's last field), and the
+# member counts that kernel serves (OSGPU_TEAM_LDS_MIN_P, OSGPU_TEAM_LDS_MAX_P)
 TEAM_LDS_U = 2
+TEAM_LDS_P = (2, 4)
 for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
@@ -128,7 +130,7 @@ def live_traffic(n, members=(2, 4, 8), reps=5, timeout=120):
         return {"_error": "rocprofv3 not on PATH"}
     keys = {"combine_vec_kernel<double, 0, 2>": 24}
     for P in members:
-        keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if 3 <= P <= 4
+        keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1]
               else f"team_vec_kernel<double, 0, {P}, true>")] = 16 * P
     tmp = tempfile.mkdtemp(prefix="osgpu_pmc_")
     dirs = {}
@@ -518,7 +520,7 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
 def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
     registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>,
-    team_lds_kernel<double,SUM,P> at 3 and 4 members
+    team_lds_kernel<double,SUM,P> at 2 to 4 members (TEAM_LDS_P)
     through the C ABI (osgpu_team_combine), one launch over all n elements --
     the work the P PEs' shard launches of a P-PE call do together: reads
     every source once, writes every target (PE q: x_q + the others in
@@ -595,8 +597,8 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     kavg_again = span_per_launch(torch, st, launch, reps)
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
-    # kernel (U = TEAM_LDS_U) at 3 and 4 members, the register kernel otherwise
-    lds = 3 <= P <= 4
+    # kernel (U = TEAM_LDS_U) at 2 to 4 members, the register kernel otherwise
+    lds = TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1]
     kern = (f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if lds    # (PMC files' key)
             else f"team_vec_kernel<double, 0, {P}, true>")
     tr = load_traffic(kern, n)
@@ -1535,7 +1537,8 @@ def bench_multi(args):
         res["roofline"] = {
             "bound": "xgmi", "achieved": per_dir, "peak": peak, "unit": "GB/s",
             "frac": per_dir / peak, "traffic": None,
-            "kernel": (f"osgpu::team_lds_kernel<double, SUM, {world}>" if 3 <= world <= 4
+            "kernel": (f"osgpu::team_lds_kernel<double, SUM, {world}>"
+                       if TEAM_LDS_P[0] <= world <= TEAM_LDS_P[1]
                        else f"osgpu::team_vec_kernel<double, SUM, {world}>"),
             "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
                      f"second: the shard reads from every peer plus every peer's writes of its "

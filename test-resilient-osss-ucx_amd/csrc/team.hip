@@ -73,7 +73,12 @@ constexpr int kTeamBlock = 256;
 #define OSGPU_TEAM_PEROUT 1
 #endif
 // from this many members on: the LDS-staged kernel (team_lds_kernel), one
-// wave per member, OSGPU_TEAM_LDS_U 16-B vectors per lane per tile.  U = 2
+// wave per member.  2 members too: against the register form on the same
+// fresh allocations it ran 1.03x faster for double sum (20 allocations on
+// two leases, median 0.794 against 0.769 of 8 TB/s) and 1.00-1.07x for every
+// (type, op) probed -- float sum/prod, double max, int sum, long xor, short
+// min, complex sum/prod (profiles/r05_team_p2_ab.jsonl).
+// OSGPU_TEAM_LDS_U 16-B vectors per lane per tile.  U = 2
 // (2 KiB per member per workgroup): timed against U = 4 in one process on
 // the same fresh allocations (tools/team_inproc_ab.py, 10 allocations per
 // member count on each of two leases, profiles/r05_team_p34_ab.jsonl) it ran
@@ -83,7 +88,7 @@ constexpr int kTeamBlock = 256;
 // from a sweep on one box: r04_team_sweep_3.jsonl.)  U = 8, 64 KiB of LDS
 // per workgroup at 8 members: 0.44-0.62, r04_team_sweep_2.jsonl
 #ifndef OSGPU_TEAM_LDS_MIN_P
-#define OSGPU_TEAM_LDS_MIN_P 3
+#define OSGPU_TEAM_LDS_MIN_P 2
 #endif
 // ... up to this many members; above, the register form.  On boxes whose
 // P-range copy itself is fast (0.81-0.84 of 8 TB/s) the register form led

@@ -126,3 +126,6 @@ def test_bench_names_the_shipped_lds_tile():
     src = open(os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc", "team.hip")).read()
     m = re.search(r"#ifndef OSGPU_TEAM_LDS_U\s*\n#define OSGPU_TEAM_LDS_U (\d+)", src)
     assert m and int(m.group(1)) == bench.TEAM_LDS_U
+    lo = re.search(r"#define OSGPU_TEAM_LDS_MIN_P (\d+)", src)
+    hi = re.search(r"#define OSGPU_TEAM_LDS_MAX_P (\d+)", src)
+    assert (int(lo.group(1)), int(hi.group(1))) == bench.TEAM_LDS_P
