@@ -48,6 +48,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # member counts that kernel serves (OSGPU_TEAM_LDS_MIN_P, OSGPU_TEAM_LDS_MAX_P)
 TEAM_LDS_U = 2
 TEAM_LDS_P = (2, 4)
+# the headline kernel: combine.hip's LDS-staged form at K = 2 inputs
+# (OSGPU_COMBINE_LDS_U2 = 2 vectors per lane), its rocprof / PMC key and label
+COMBINE_KERNEL = "combine_lds_kernel<double, 0, 2, 2>"
+COMBINE_LABEL = "osgpu::combine_lds_kernel<double, SUM, 2, 2>"
 for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, sub))
 
@@ -91,7 +95,7 @@ def parse():
 LIVE_TRAFFIC = {}  # filled by live_traffic() before the line's rooflines are built
 
 
-def load_traffic(kernel="combine_vec_kernel<double, 0, 2>", n=None):
+def load_traffic(kernel=COMBINE_KERNEL, n=None):
     """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters:
     this run's own passes (LIVE_TRAFFIC) when they produced the kernel, else
     the newest profiles/*traffic*.json (tools/pmc_traffic.py) covering that
@@ -128,7 +132,7 @@ def live_traffic(n, members=(2, 4, 8), reps=5, timeout=120):
     prof = shutil.which("rocprofv3")
     if not prof:
         return {"_error": "rocprofv3 not on PATH"}
-    keys = {"combine_vec_kernel<double, 0, 2>": 24}
+    keys = {COMBINE_KERNEL: 24}
     for P in members:
         keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1]
               else f"team_vec_kernel<double, 0, {P}, true>")] = 16 * P
@@ -964,7 +968,7 @@ def bench_single(args):
         "frac": B / kavg / 1e9 / HBM_PEAK_GBS,
         "traffic": tr.get("bytes_per_launch") if tr else None,
         "traffic_source": tr.get("source") if tr else None,
-        "kernel": "osgpu::combine_vec_kernel<double, SUM, 2>",
+        "kernel": COMBINE_LABEL,
         "kernel_avg_us": kavg * 1e6,
         "kernel_avg_how": "HIP event span over the K timed launches on the launch stream / K",
         "kernel_median_us_per_launch_events": kms[len(kms) // 2] * 1e3,
@@ -1604,7 +1608,7 @@ def bench_multi(args):
                 "frac_of_8TBs_per_gpu": args.steps * 3 * n * 8 / tl / 1e9 / HBM_PEAK_GBS,
                 "correct_sample_all_ranks": _agree(dist, world, ok),
                 "note": "NOT a to_all (no exchange, no scaling claim): "
-                        "combine_vec_kernel<double,SUM,2> on every GPU at once, 3*nreduce*8 B "
+                        "combine_lds_kernel<double,SUM,2,2> on every GPU at once, 3*nreduce*8 B "
                         "per GPU per step, max-over-ranks time -- the per-GPU fold rate while "
                         "all GPUs stream"}
             del lout

@@ -153,6 +153,69 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
     }
 }
 
+// LDS-staged form (OSGPU_COMBINE_LDS, 2 <= K <= OSGPU_COMBINE_LDS_MAX_K): K
+// waves per workgroup, a tile of 64*U 16-B vectors of every input.  Wave k
+// streams input k's tile into LDS (one read stream per wave, like the copy
+// kernel and team_lds_kernel); after the barrier the K waves fold the tile
+// from LDS in input order and store it, each a contiguous 1 KiB per
+// instruction.  HBM bytes as combine_vec_kernel.  Timed against it in one
+// process on the same fresh arrays (tools/combine_inproc_ab.py, 6
+// allocations each, profiles/r05_combine_lds_ab.jsonl): double sum K = 2
+// 1.04x with U = 2 (0.824 against 0.792 of 8 TB/s median; 1.02x with
+// U = 4), K = 3 and 4 1.02x with U = 4 (U = 2: 1.01x, 0.98x); float / int
+// sum 1.02x / 1.04x, long xor 1.01x, double max 1.00x at K = 2.
+#ifndef OSGPU_COMBINE_LDS
+#define OSGPU_COMBINE_LDS 1
+#endif
+#ifndef OSGPU_COMBINE_LDS_MAX_K
+#define OSGPU_COMBINE_LDS_MAX_K 4
+#endif
+#ifndef OSGPU_COMBINE_LDS_U2
+#define OSGPU_COMBINE_LDS_U2 2  // vectors per lane per input at K = 2
+#endif
+#ifndef OSGPU_COMBINE_LDS_U
+#define OSGPU_COMBINE_LDS_U 4   // ... at K = 3, 4
+#endif
+
+template <typename T, int OP, int K, int U>
+__global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K> in, size_t nvec,
+                                                              size_t head, size_t tail_start,
+                                                              int nedge)
+{
+    constexpr int V = 64 * U;  // vectors per input per tile
+    __shared__ u32x4 tile[K][V];
+    if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
+        size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
+        out[e] = fold_scalar<T, OP, K>(in, e);
+    }
+    const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
+    const int lane = (int) (threadIdx.x & 63);
+    const size_t base = (size_t) blockIdx.x * V;
+    const bool whole = base + V <= nvec;
+    const T *pw = in.p[0];
+#pragma unroll
+    for (int k = 1; k < K; k++)
+        if (w == k) pw = in.p[k];
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(pw + head);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (whole || base + u * 64 + lane < nvec)
+            v[u] = __builtin_nontemporal_load(src + base + u * 64 + lane);
+#pragma unroll
+    for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
+    __syncthreads();
+    u32x4 *dst = reinterpret_cast<u32x4 *>(out + head);
+    for (int j = (int) threadIdx.x; j < V; j += 64 * K) {
+        if (!whole && base + j >= nvec) continue;
+        Vec16<T> x[K], r;
+#pragma unroll
+        for (int k = 0; k < K; k++) x[k].v = tile[k][j];
+        fold_vec<T, OP, K>(x, r);
+        __builtin_nontemporal_store(r.v, dst + base + j);
+    }
+}
+
 // Element-granular fallback for inputs whose 16-byte phases differ.
 template <typename T, int OP, int K>
 __global__ __launch_bounds__(kBlock) void combine_scalar_kernel(T *out, Inputs<T, K> in,
@@ -190,6 +253,15 @@ static hipError_t launch_k(T *out, const T *const *srcs, size_t n, hipStream_t s
     size_t nvec = (n - head) / W;
     size_t tail_start = head + nvec * W;
     int nedge = (int) (head + (n - tail_start));
+    if constexpr (OSGPU_COMBINE_LDS && K >= 2 && K <= OSGPU_COMBINE_LDS_MAX_K) {
+        constexpr int UL = K == 2 ? OSGPU_COMBINE_LDS_U2 : OSGPU_COMBINE_LDS_U;
+        size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
+        if (blocks == 0) blocks = 1;
+        if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((combine_lds_kernel<T, OP, K, UL>), dim3((unsigned) blocks),
+                           dim3(64 * K), 0, s, out, in, nvec, head, tail_start, nedge);
+        return hipGetLastError();
+    }
     size_t per_block = (size_t) kBlock * U;
     size_t blocks = (nvec + per_block - 1) / per_block;
     if (blocks == 0) blocks = 1;

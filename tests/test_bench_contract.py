@@ -129,3 +129,8 @@ def test_bench_names_the_shipped_lds_tile():
     lo = re.search(r"#define OSGPU_TEAM_LDS_MIN_P (\d+)", src)
     hi = re.search(r"#define OSGPU_TEAM_LDS_MAX_P (\d+)", src)
     assert (int(lo.group(1)), int(hi.group(1))) == bench.TEAM_LDS_P
+    comb = open(os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc", "combine.hip")).read()
+    on = re.search(r"#define OSGPU_COMBINE_LDS (\d+)", comb)
+    u2 = re.search(r"#define OSGPU_COMBINE_LDS_U2 (\d+)", comb)
+    assert on and int(on.group(1)) == 1
+    assert u2 and bench.COMBINE_KERNEL == f"combine_lds_kernel<double, 0, 2, {u2.group(1)}>"

@@ -48,7 +48,7 @@ def test_bench_labels_looked_up_traffic():
     bench.LIVE_TRAFFIC.clear()
     tr = bench.load_traffic(n=64 << 20)
     assert tr is not None and tr["source"].startswith("looked up: profiles/")
-    bench.LIVE_TRAFFIC["combine_vec_kernel<double, 0, 2>"] = {"nreduce": 64 << 20,
+    bench.LIVE_TRAFFIC[bench.COMBINE_KERNEL] = {"nreduce": 64 << 20,
                                                               "source": "live", "bytes_per_launch": 1}
     try:
         assert bench.load_traffic(n=64 << 20)["source"] == "live"

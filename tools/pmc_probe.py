@@ -8,7 +8,7 @@ looked up from profiles/.  Every launch goes through the C ABI of the
 in-tree library (osgpu_combine / osgpu_team_combine), on the same shapes the
 bench times:
 
-  combine  combine_vec_kernel<double, SUM, 2>: 2 sources -> 1 target, n doubles
+  combine  combine_lds_kernel<double, SUM, 2, 2>: 2 sources -> 1 target, n doubles
   team P   the team kernel for P members (double sum, team.hip's form for P),
            P sources -> P targets, n doubles each
 

@@ -24,7 +24,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "combine_vec_kernel<double, 0, 2>"
+KERNEL = "combine_lds_kernel<double, 0, 2, 2>"  # bench.COMBINE_KERNEL
 METHOD = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 "
           "(gfx950 half-count on 16-B streaming reads), KiB -> bytes, median over launches")
 
