@@ -163,18 +163,20 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
 // allocations each, profiles/r05_combine_lds_ab.jsonl): double sum K = 2
 // 1.04x with U = 2 (0.824 against 0.792 of 8 TB/s median; 1.02x with
 // U = 4), K = 3 and 4 1.02x with U = 4 (U = 2: 1.01x, 0.98x); float / int
-// sum 1.02x / 1.04x, long xor 1.01x, double max 1.00x at K = 2.
+// sum 1.02x / 1.04x, long xor 1.01x, double max 1.00x at K = 2; K = 5 and
+// 8 (32 Mi doubles) 1.04x and 1.07x with U = 4 (U = 2: 1.01x, 1.05x); at
+// 8 / 64 / 128 Mi doubles, K = 2: 1.07x / 1.04x / 1.04x.
 #ifndef OSGPU_COMBINE_LDS
 #define OSGPU_COMBINE_LDS 1
 #endif
 #ifndef OSGPU_COMBINE_LDS_MAX_K
-#define OSGPU_COMBINE_LDS_MAX_K 4
+#define OSGPU_COMBINE_LDS_MAX_K 8
 #endif
 #ifndef OSGPU_COMBINE_LDS_U2
 #define OSGPU_COMBINE_LDS_U2 2  // vectors per lane per input at K = 2
 #endif
 #ifndef OSGPU_COMBINE_LDS_U
-#define OSGPU_COMBINE_LDS_U 4   // ... at K = 3, 4
+#define OSGPU_COMBINE_LDS_U 4   // ... at K = 3 .. 8
 #endif
 
 template <typename T, int OP, int K, int U>
