@@ -55,6 +55,15 @@ constexpr int kTeamBlock = 256;
 #ifndef OSGPU_TEAM_G8
 #define OSGPU_TEAM_G8 2
 #endif
+// ... for the real (non-complex) types: one round of all U = 4 vectors
+// (their loads all in flight before the first fold; 3-6 waves per SIMD, no
+// scratch).  Against G = 2 in one process on the same allocations
+// (tools/team_inproc_ab.py, profiles/r05_team_p8_tile_ab.jsonl): 1.006x
+// over 7 (type, op) pairs at 5-8 members, floating-point folds 1.00-1.03x,
+// integer ones 0.996-1.004x.  The complex sum keeps G = 2 (G = 4 spills it)
+#ifndef OSGPU_TEAM_G8R
+#define OSGPU_TEAM_G8R 4
+#endif
 // the register-heavy folds above 4 members (complex products: 4-6 VALU
 // temporaries per element per output) take rounds of OSGPU_TEAM_GH vectors
 #ifndef OSGPU_TEAM_GH
@@ -68,6 +77,20 @@ constexpr int kTeamBlock = 256;
 // the integer ones (profiles/r04_team_type_op_sweep.jsonl)
 #ifndef OSGPU_TEAM_PIPE
 #define OSGPU_TEAM_PIPE 1
+#endif
+// floating-point folds on the two-buffer pipeline too: round 4 lost 0.2-0.4
+// of the rate to it because fold_store was not inlined and the round buffers
+// went to scratch; with the lambdas forced inline it compiles clean, and at
+// U = 6 / 8 (3 / 4 rounds of 2) ran 0.97-0.98x of the shipped tile (same
+// A/B file), so it stays off
+#ifndef OSGPU_TEAM_PIPE_FP
+#define OSGPU_TEAM_PIPE_FP 0
+#endif
+#ifndef OSGPU_TEAM_PIPE_FENCE
+#define OSGPU_TEAM_PIPE_FENCE 0
+#endif
+#ifndef OSGPU_TEAM_OCC_LDS
+#define OSGPU_TEAM_OCC_LDS 0
 #endif
 #ifndef OSGPU_TEAM_PEROUT
 #define OSGPU_TEAM_PEROUT 1
@@ -128,8 +151,10 @@ struct TeamShape {
     static constexpr bool kHeavy = (std::is_same<T, cfloat>::value || std::is_same<T, cdouble>::value) &&
                                    OP == OP_PROD;
     static constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
-    static constexpr int G = P <= 4 ? U : (kHeavy ? OSGPU_TEAM_GH : OSGPU_TEAM_G8);
-    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1 && std::is_integral<T>::value;
+    static constexpr bool kComplex = std::is_same<T, cfloat>::value || std::is_same<T, cdouble>::value;
+    static constexpr int G = P <= 4 ? U : (kHeavy ? OSGPU_TEAM_GH : (kComplex ? OSGPU_TEAM_G8 : OSGPU_TEAM_G8R));
+    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1 &&
+                                  (std::is_integral<T>::value || OSGPU_TEAM_PIPE_FP);
     // ordered folds above 4 members: fold, check and store one output at a
     // time instead of all P outputs, then all P stores
     static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
@@ -204,6 +229,16 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
     constexpr int W = 16 / sizeof(T);
     using S = TeamShape<T, OP, P>;
     constexpr int U = S::U;
+#if OSGPU_TEAM_OCC_LDS
+    // occupancy cap (experiment): a workgroup holds this much LDS, so at
+    // most 160 KiB / OSGPU_TEAM_OCC_LDS workgroups share a CU.  3 or 4
+    // workgroups per CU at 6 / 8 members: 0.99-1.00x (same A/B file)
+    if constexpr (P > 4) {
+        __shared__ unsigned occ_pad[OSGPU_TEAM_OCC_LDS / 4];
+        if (nvec == 0) reinterpret_cast<volatile unsigned *>(occ_pad)[threadIdx.x] = 0;
+        __syncthreads();
+    }
+#endif
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -221,7 +256,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
     // hold a NaN part (rare; elem_ops.hpp Fast) -- no branch per element, so
     // the tile's loads stay in flight ahead of the folds
     using F = Fast<T, OP>;
-    auto fold_store = [&](TVec<T> (&in)[P], size_t j) {
+    auto fold_store = [&](TVec<T> (&in)[P], size_t j) __attribute__((always_inline)) {
         if constexpr (ORDERED && S::kPerOutput) {
             // one output at a time: fold, check, store -- only one output
             // vector live beside the inputs
@@ -288,7 +323,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         // TeamShape's G (all 4*P at once spills the 8-input complex sum)
         constexpr int G = S::G;
         constexpr int R = U / G;
-        auto load_round = [&](TVec<T> (&in)[G][P], int g) {
+        auto load_round = [&](TVec<T> (&in)[G][P], int g) __attribute__((always_inline)) {
 #pragma unroll
             for (int u = 0; u < G; u++)
 #pragma unroll
@@ -305,7 +340,12 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                 constexpr int r = decltype(rc)::value;
                 auto &cur = (r % 2 == 0) ? b0 : b1;
                 auto &nxt = (r % 2 == 0) ? b1 : b0;
-                if constexpr (r + 1 < R) load_round(nxt, r + 1);
+                if constexpr (r + 1 < R) {
+                    load_round(nxt, r + 1);
+                    // keep the scheduler from sinking these loads below the
+                    // stores (it does, to save registers, when it may)
+                    if constexpr (OSGPU_TEAM_PIPE_FENCE) asm volatile("" ::: "memory");
+                }
 #pragma unroll
                 for (int u = 0; u < G; u++) fold_store(cur[u], t0 + (size_t) (r * G + u) * kTeamBlock);
             });
