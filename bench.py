@@ -61,6 +61,112 @@ GIB = float(1 << 30)
 METRIC = "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2/4/8 GPU"
 
 
+# --------------------------------------------------------------------------
+# the printed line: at most LINE_CAP bytes (the driver reads one JSON line of
+# bounded size; round 5's 21.7 KB line went unparsed).  The full result --
+# placements with addresses, sweeps, per-rank reports, notes -- goes to the
+# detail file named in the line; the line keeps every contract field plus a
+# summary (min / median / max, no address lists) of each side measurement.
+# --------------------------------------------------------------------------
+
+LINE_CAP = 8192
+# keys whose values stay in the detail file only (anywhere in the tree)
+DETAIL_ONLY = frozenset((
+    "addresses", "placements", "sweep", "heap_preflight", "ranks", "note", "how", "what",
+    "kernel_avg_how", "placements_note", "crossover_note", "hip_runtime", "offset_in_2MiB",
+    "peak_measured_how", "bytes_convention", "rule", "copy_ceiling_same_mix",
+    "after_timed_region_100_launches", "copy_ceiling_same_bytes", "traffic_source",
+    "dma_state", "dma_state_after", "element_ops", "path_mode", "launch_note"))
+# strings that keep their full text (up to 480 characters)
+LONG_OK = frozenset(("metric", "workload", "sample", "incomplete", "detail"))
+# top-level keys dropped, in this order, while the line is still over the cap
+DROP_ORDER = ("host_staged_in_torch_process", "cpu_baseline_configs", "traffic_live",
+              "api", "collectives", "longdouble_team_8_members", "config3_long_bitwise_256MiB",
+              "north_star_double_sum_128Mi", "config5_host_staged", "host_staged",
+              "roofline_call", "small_call", "team_by_members", "local_fold_no_exchange",
+              "team_push", "xgmi_probe", "small_calls", "config5",
+              "rccl_integer_auto", "launch", "config4", "rccl", "hbm_aggregate")
+
+
+def _shrink(x, key=None):
+    """The line's form of one value: DETAIL_ONLY keys removed, floats to 5
+    significant digits, long strings cut, lists of more than 16 items cut."""
+    if isinstance(x, dict):
+        return {k: _shrink(v, k) for k, v in x.items() if k not in DETAIL_ONLY}
+    if isinstance(x, (list, tuple)):
+        return [_shrink(v) for v in x[:16]]
+    if isinstance(x, float):
+        return float(f"{x:.5g}") if x == x and abs(x) != float("inf") else None
+    if isinstance(x, str):
+        lim = 480 if key in LONG_OK else 160
+        return x if len(x) <= lim else x[:lim - 3] + "..."
+    return x
+
+
+def _sum_cpu_configs(v):
+    out = {k: v[k] for k in ("kind", "cpus_allowed") if k in v}
+    for name in ("config3", "config4", "config5"):
+        c = v.get(name)
+        if isinstance(c, dict):
+            out[name] = {op: c[op]["GiBs_per_PE"] for op in c
+                         if isinstance(c[op], dict) and "GiBs_per_PE" in c[op]}
+            out[name]["pes"] = c.get("pes")
+            if "error" in c:
+                out[name]["error"] = c["error"]
+    return out
+
+
+def _sum_torch_staged(v):
+    return {k: v[k].get("pcie_GBs_each_way") if isinstance(v.get(k), dict) else v.get(k)
+            for k in ("pinned", "pageable", "error") if k in v}
+
+
+# top-level side measurements given a purpose-made summary in the line
+SUMMARIZERS = {"cpu_baseline_configs": _sum_cpu_configs,
+               "host_staged_in_torch_process": _sum_torch_staged}
+
+
+def fit_line(res, detail_path=None, cap=LINE_CAP):
+    """The JSON line for `res` (<= cap bytes) and, when detail_path is given,
+    the full `res` written there first (named in the line as `detail`)."""
+    if detail_path:
+        try:
+            os.makedirs(os.path.dirname(detail_path) or ".", exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(res, f, indent=1, default=str)
+            res = dict(res, detail=os.path.relpath(detail_path, ROOT))
+        except OSError as e:  # the line still prints
+            res = dict(res, detail=f"not written: {e}"[:200])
+    line = {}
+    for k, v in res.items():
+        try:
+            line[k] = _shrink(SUMMARIZERS[k](v) if k in SUMMARIZERS and isinstance(v, dict) else v, k)
+        except Exception as e:  # a summary must never cost the line
+            line[k] = {"summary_error": repr(e)[:120]}
+    dropped = []
+    text = json.dumps(line, separators=(",", ":"))
+    for k in DROP_ORDER:
+        if len(text) <= cap:
+            break
+        if k in line:
+            del line[k]
+            dropped.append(k)
+            line["dropped_to_fit"] = dropped
+            text = json.dumps(line, separators=(",", ":"))
+    if len(text) > cap:   # last resort: the contract fields alone
+        keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline", "cpu_baseline", "detail", "incomplete")
+        line = {k: line[k] for k in keep if k in line}
+        line["dropped_to_fit"] = "all side measurements (see detail)"
+        text = json.dumps(line, separators=(",", ":"))
+    return text
+
+
+def default_detail(n_gpus):
+    return os.path.join(ROOT, "gpurun_out", f"bench_detail_n{n_gpus}.json")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +188,9 @@ def parse():
     ap.add_argument("--no-api", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=64 << 20,
                     help="nreduce of the CPU-baseline sample")
+    ap.add_argument("--detail", default=None,
+                    help="where the full result goes (default gpurun_out/bench_detail_n<N>.json); "
+                         "the printed line is its <= 8 KiB summary")
     ap.add_argument("--dry-ranks", action="store_true",
                     help="N>1 launcher check without the GPU (tests/test_bench_contract.py)")
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
@@ -364,8 +473,9 @@ def host_staged_child(n, timeout=240, what="host_staged_time(%d)"):
     copies pick an engine mask of both SDMA engines when both are idle; the
     copy is refused and redone as a blit kernel ("HSA copy failed with code
     4097, falling to Blit copy", profiles/r05_torch_runtime_d2h.txt), which
-    caps the duplex pair at 41.9 GB/s each way and, inside the staged
-    pipeline, at 27-35 depending on timing.  The 7.2 runtime picks one
+    caps the duplex pair at 41.9 GB/s each way; the staged pipeline in the
+    torch process measured 44.4 pinned / 39.6 pageable in round 5 (DESIGN
+    history 15.1), beside 44.5 / 41.3 here.  The 7.2 runtime picks one
     engine per direction (48.3 each way)."""
     import subprocess
     code = ("import sys, json; sys.path.insert(0, %r); import bench; "
@@ -446,7 +556,9 @@ def collectives_single(P=4, nb=64 << 20, reps=10):
     out["fcollect64_device"] = {"pes": P, "bytes_per_pe": nb, "ms_per_call": t * 1e3,
                                 "GBps_all_pes": CB.moved("fcollect", P, nb) / t / 1e9}
     # host symmetric heaps (pageable): the STAGED path, H2D / exchange / D2H
-    # pipelined over two slots; the P PEs share this GPU's PCIe link
+    # one after the other per chunk (a two-slot pipeline was measured and
+    # reverted: profiles/r05_coll_staged_pipeline_ab.jsonl); the P PEs share
+    # this GPU's PCIe link
     nh = nb // 4
     t = CB.api_time("fcollect", P, nh, 5, False)
     out["fcollect64_host_staged"] = {
@@ -521,28 +633,18 @@ def kernel_rate(L, torch, type_code, op_code, n, esz, dtype, fill, reps=20):
     return span_per_launch(torch, st, launch, reps), a, b, out
 
 
-def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
-    """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
-    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>,
-    team_lds_kernel<double,SUM,P> at 2 to 4 members (TEAM_LDS_P)
-    through the C ABI (osgpu_team_combine), one launch over all n elements --
-    the work the P PEs' shard launches of a P-PE call do together: reads
-    every source once, writes every target (PE q: x_q + the others in
-    ascending order).  Algorithmic bytes 2*P*n*8 per launch.  HIP events on
-    the launch stream.  Beside it the same-mix ceiling: the copy kernel
-    (csrc/copy.hip) moving P ranges of n*8 bytes in one launch, its tiles
-    dealt round-robin over the ranges -- P read and P write streams at once
-    over the same bytes, nothing folded.
-    layout "alloc": every array its own allocation; "symheap": P symmetric
-    heaps carved back to back out of ONE allocation (as PE threads' heaps in
-    one buffer), member p's source at offset 0 of heap p and its target at
-    n*8 + 2 MiB: every array shares its low 21 address bits and the regular
-    high bits of one allocation -- the worst layout the sweep found
-    (tools/team_layout_sweep.py symheap, profiles/r05_team_symheap.jsonl);
+def team_arrays(torch, n, P, layout="alloc", seed=0):
+    """P sources (uniform [1,2) doubles) and P targets of n doubles for the
+    team kernel.  layout "alloc": every array its own allocation; "symheap":
+    P symmetric heaps carved back to back out of ONE allocation (as PE
+    threads' heaps in one buffer), member p's source at offset 0 of heap p
+    and its target at n*8 + 2 MiB: every array shares its low 21 address bits
+    and the regular high bits of one allocation -- the worst layout the sweep
+    found (tools/team_layout_sweep.py symheap, profiles/r05_team_symheap.jsonl);
     heaps from osgpu_heap_create (one allocation each) do not show it
     (profiles/r05_heap_stagger_ab.jsonl)."""
     dev = torch.device("cuda:0")
-    g = torch.Generator(device=dev).manual_seed(11 + P)
+    g = torch.Generator(device=dev).manual_seed(11 + P + 100 * seed)
     if layout == "symheap":
         heap = (2 * n * 8 + (4 << 20) + (2 << 20) - 1) // (2 << 20) * (2 << 20)
         buf = torch.empty(P * heap + (2 << 20), dtype=torch.uint8, device=dev)
@@ -556,11 +658,66 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
         srcs_t = [torch.empty(n, dtype=torch.float64, device=dev).uniform_(1.0, 2.0, generator=g)
                   for _ in range(P)]
         dsts_t = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(P)]
+    return srcs_t, dsts_t
+
+
+class Canary:
+    """A fixed-buffer control: the copy kernel over two arrays allocated once,
+    before the first placement trial, and never freed until the end.  Timed
+    right before and right after every trial: a slow trial whose canary is
+    slow too was the box slowing down in time (a transient); a slow trial
+    with a normal canary was its own placement."""
+
+    def __init__(self, L, torch, nbytes=512 << 20, reps=10):
+        dev = torch.device("cuda:0")
+        self.torch, self.L, self.reps, self.nbytes = torch, L, reps, nbytes
+        self.a = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(3)
+        self.o = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.st = torch.cuda.Stream(device=dev)
+        self.sp = ctypes.c_void_p(self.st.cuda_stream)
+        self.D = (ctypes.c_void_p * 1)(self.o.data_ptr())
+        self.S = (ctypes.c_void_p * 1)(self.a.data_ptr())
+        self.N = (ctypes.c_size_t * 1)(nbytes)
+        self.samples = []
+        self()
+
+    def __call__(self):
+        def launch():
+            assert self.L.osgpu_copy(self.D, self.S, self.N, 1, self.sp) == 0
+        launch()
+        t = span_per_launch(self.torch, self.st, launch, self.reps)
+        f = 2 * self.nbytes / t / 1e9 / HBM_PEAK_GBS
+        self.samples.append(f)
+        return f
+
+    def reference(self):
+        v = sorted(self.samples)
+        return v[len(v) // 2]
+
+
+def team_kernel_rate(L, torch, n, reps, P=2, arrays=None, layout="alloc", canary=None):
+    """The kernel shmem_double_sum_to_all actually dispatches on one GPU with
+    registered heaps (TEAM path, csrc/team.hip): team_vec_kernel<double,SUM,P>,
+    team_lds_kernel<double,SUM,P> at 2 to 4 members (TEAM_LDS_P)
+    through the C ABI (osgpu_team_combine), one launch over all n elements --
+    the work the P PEs' shard launches of a P-PE call do together: reads
+    every source once, writes every target (PE q: x_q + the others in
+    ascending order).  Algorithmic bytes 2*P*n*8 per launch.  HIP events on
+    the launch stream.  Beside it the same-mix ceiling: the copy kernel
+    (csrc/copy.hip) moving P ranges of n*8 bytes in one launch, its tiles
+    dealt round-robin over the ranges -- P read and P write streams at once
+    over the same bytes, nothing folded.  `arrays` (team_arrays) are made
+    here when not given; `canary` (Canary) is timed right before and right
+    after this trial's own timings."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(77 + P)
+    srcs_t, dsts_t = arrays if arrays is not None else team_arrays(torch, n, P, layout)
     st = torch.cuda.Stream(device=dev)
     srcs = (ctypes.c_void_p * P)(*[x.data_ptr() for x in srcs_t])
     dsts = (ctypes.c_void_p * P)(*[x.data_ptr() for x in dsts_t])
     sp = ctypes.c_void_p(st.cuda_stream)
     torch.cuda.synchronize()
+    can_before = canary() if canary is not None else None
 
     def launch():
         if L.osgpu_team_combine(5, 0, P, dsts, srcs, n, sp) != 0:
@@ -599,6 +756,7 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
     # the team kernel again on the same arrays after the copy: a slow first
     # timing that is fast here was a transient of the box, not the placement
     kavg_again = span_per_launch(torch, st, launch, reps)
+    can_after = canary() if canary is not None else None
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
     # kernel (U = TEAM_LDS_U) at 2 to 4 members, the register kernel otherwise
@@ -622,7 +780,9 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
            "copy_ceiling_same_mix": {"kernel": "copy_vec_kernel (ranges dealt round-robin)",
                                      "ranges": P, "bytes_per_range": n * 8, "us": cavg * 1e6,
                                      "frac_of_8TBs": cfrac},
+           "copy_frac": cfrac,
            "frac_of_copy_ceiling": frac / cfrac,
+           "canary_before": can_before, "canary_after": can_after,
            # where the arrays landed (virtual; each a separate allocation):
            # base addresses and their offsets within a 2 MiB fragment
            "addresses": {"src": [hex(x.data_ptr()) for x in srcs_t],
@@ -630,49 +790,85 @@ def team_kernel_rate(L, torch, n, reps, P=2, layout="alloc"):
                          "offset_in_2MiB": [x.data_ptr() % (2 << 20) for x in srcs_t + dsts_t]},
            "note": f"one launch over all nreduce elements = the {P} PEs' shard launches of a "
                    f"{P}-PE call; {P} reads + {P} writes of 8 B per element"}
-    del srcs_t, dsts_t
-    if layout == "symheap":
-        del buf
-    torch.cuda.empty_cache()
+    if arrays is None:
+        del srcs_t, dsts_t
+        torch.cuda.empty_cache()
     return out
 
 
-def team_placements(L, torch, n, reps, P, trials=3):
-    """team_kernel_rate on `trials` fresh allocations (the arrays freed and
-    allocated again: new physical pages).  The rate of 2P streams read and
-    written in lockstep depends on where the pages land -- the same kernel
-    and the round-robin copy both move 0.72-0.84 of 8 TB/s at P = 2..8
-    across placements (tools/tune_team.hip `layouts`,
-    profiles/r03_team_layouts.jsonl) -- so the line reports every trial and
-    the medians."""
-    runs = [team_kernel_rate(L, torch, n, reps, P) for _ in range(trials)]
+def team_placements(L, torch, n, reps, P, trials=3, canary=None):
+    """team_kernel_rate on `trials` placements, ALL allocated up front (no
+    array is freed between trials: round 5's three collapses were all trial
+    1, timed right after trial 0's arrays were freed), each trial bracketed
+    by the canary.  The rate of 2P streams read and written in lockstep
+    depends on where the pages land -- the same kernel and the round-robin
+    copy both move 0.72-0.84 of 8 TB/s at P = 2..8 across placements
+    (profiles/r03_team_layouts.jsonl) -- so the line reports every trial
+    (labelled by label_trials) and the medians."""
+    arrs = [team_arrays(torch, n, P, seed=t) for t in range(trials)]
+    runs = [team_kernel_rate(L, torch, n, reps, P, arrays=arrs[t], canary=canary)
+            for t in range(trials)]
+    del arrs
+    torch.cuda.empty_cache()
     med = sorted(runs, key=lambda r: r["frac_of_copy_ceiling"])[len(runs) // 2]
-    out = dict(med)
-    # heaps carved out of one allocation (equal low address bits, regular
-    # high ones): the worst layout measured, reported beside the placements
-    try:
-        sh = team_kernel_rate(L, torch, n, reps, P, layout="symheap")
-        out["one_allocation_heaps_layout"] = {
-            "frac": sh["frac"], "copy_frac": sh["copy_ceiling_same_mix"]["frac_of_8TBs"],
-            "frac_of_copy_ceiling": sh["frac_of_copy_ceiling"],
-            "kernel_avg_us": sh["kernel_avg_us"], "bit_exact_sample": sh["bit_exact_sample"],
-            "offset_in_2MiB": sh["addresses"]["offset_in_2MiB"]}
-    except Exception as e:  # report, never hide
-        out["one_allocation_heaps_layout"] = {"error": repr(e)[:200]}
-    out["placements"] = [{"frac": r["frac"], "copy_frac": r["copy_ceiling_same_mix"]["frac_of_8TBs"],
-                          "frac_of_copy_ceiling": r["frac_of_copy_ceiling"],
-                          "kernel_avg_us": r["kernel_avg_us"],
-                          "kernel_avg_us_again_after_copy": r["kernel_avg_us_again_after_copy"],
-                          "src": r["addresses"]["src"], "dst": r["addresses"]["dst"]}
-                         for r in runs]
+    out = {k: med[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                               "traffic_source", "kernel", "members", "nreduce",
+                               "kernel_avg_us", "algorithmic_bytes_per_launch", "copy_frac",
+                               "frac_of_copy_ceiling")}
+    out["placements"] = runs      # full records (addresses): the detail file
+    out["trials"] = [{"frac": r["frac"], "copy_frac": r["copy_frac"],
+                      "of_copy": r["frac_of_copy_ceiling"],
+                      "again_us": r["kernel_avg_us_again_after_copy"],
+                      "canary": [r["canary_before"], r["canary_after"]]} for r in runs]
     for key, get in (("frac", lambda r: r["frac"]),
                      ("frac_of_copy_ceiling", lambda r: r["frac_of_copy_ceiling"])):
         v = sorted(get(r) for r in runs)
         out[key + "_min"], out[key + "_median"], out[key + "_max"] = v[0], v[len(v) // 2], v[-1]
-    out["placements_note"] = (f"{trials} allocations; the fields above are the trial with the "
-                              f"median frac_of_copy_ceiling, *_min / *_median / *_max over all")
+    cs = sorted(c for r in runs for c in (r["canary_before"], r["canary_after"]) if c is not None)
+    if cs:
+        out["canary_min"], out["canary_median"] = cs[0], cs[len(cs) // 2]
+    out["placements_note"] = (f"{trials} placements allocated up front; the fields above are "
+                              f"the trial with the median frac_of_copy_ceiling, *_min / *_median / "
+                              f"*_max over all; canary = the fixed-buffer copy's fraction of "
+                              f"8 TB/s right before / after each trial")
     out["bit_exact_sample"] = all(r["bit_exact_sample"] for r in runs)
+    # heaps carved out of one allocation (equal low address bits, regular
+    # high ones): the worst layout measured, reported beside the placements
+    try:
+        sh = team_kernel_rate(L, torch, n, reps, P, layout="symheap", canary=canary)
+        out["one_allocation_heaps_layout"] = {
+            "frac": sh["frac"], "copy_frac": sh["copy_frac"],
+            "frac_of_copy_ceiling": sh["frac_of_copy_ceiling"],
+            "bit_exact_sample": sh["bit_exact_sample"]}
+    except Exception as e:  # report, never hide
+        out["one_allocation_heaps_layout"] = {"error": repr(e)[:200]}
     return out
+
+
+def label_trials(by_members, canary_ref, slow=0.9, box=0.9):
+    """Every placement trial labelled: "ok", or -- when its frac or its copy's
+    falls below `slow` x its member count's median -- "transient" (a canary
+    sample around it below `box` x the run's canary median: the box was
+    slow at that time) or "placement" (the canary was normal: the arrays'
+    placement itself was slow).  Returns the count of each label."""
+    counts = {"ok": 0, "transient": 0, "placement": 0}
+    for rec in by_members.values():
+        tr = rec.get("trials") if isinstance(rec, dict) else None
+        if not tr:
+            continue
+        fm = sorted(t["frac"] for t in tr)[len(tr) // 2]
+        cm = sorted(t["copy_frac"] for t in tr)[len(tr) // 2]
+        for t in tr:
+            is_slow = t["frac"] < slow * fm or t["copy_frac"] < slow * cm
+            cmin = min((c for c in t["canary"] if c is not None), default=None)
+            if not is_slow:
+                t["label"] = "ok"
+            elif cmin is not None and canary_ref and cmin < box * canary_ref:
+                t["label"] = "transient"
+            else:
+                t["label"] = "placement"
+            counts[t["label"]] += 1
+    return counts
 
 
 def stream_ceiling(L, torch, nbytes, reps=20):
@@ -985,17 +1181,27 @@ def bench_single(args):
     # the kernel the API dispatches (TEAM path), under the same roofline, for
     # 2, 4 and 8 members (config 4's 8 PEs on one GPU run it at P = 8), each
     # beside the copy kernel moving the same P read + P write streams
+    res["team_by_members"] = {}
+    canary = None
     try:
-        res["roofline_team"] = team_kernel_rate(L, torch, n, args.steps)
-    except Exception as e:  # report, never hide
-        res["roofline_team"] = {"error": repr(e)}
-    res["roofline_team_by_members"] = {}
-    for P in ((2, 4, 8) if not args.no_extra else ()):
+        canary = Canary(L, torch)
+    except Exception as e:  # report, never hide; the trials run without it
+        res["team_by_members"]["canary_error"] = repr(e)[:200]
+    for P in ((2, 4, 8) if not args.no_extra else (2,)):
         try:
-            res["roofline_team_by_members"][str(P)] = team_placements(
-                L, torch, n, min(args.steps, 20), P)
+            res["team_by_members"][str(P)] = team_placements(
+                L, torch, n, min(args.steps, 20), P, canary=canary)
         except Exception as e:  # report, never hide
-            res["roofline_team_by_members"][str(P)] = {"error": repr(e)}
+            res["team_by_members"][str(P)] = {"error": repr(e)}
+    if canary is not None:
+        ref = canary.reference()
+        res["team_by_members"]["canary"] = {
+            "what": "copy_vec_kernel over 2 x 512 MiB allocated once before the first trial, "
+                    "fraction of 8 TB/s, timed right before and after every trial",
+            "median": ref, "min": min(canary.samples), "max": max(canary.samples),
+            "labels": label_trials(res["team_by_members"], ref)}
+        del canary
+        torch.cuda.empty_cache()
     if not args.no_api:
         try:
             res["api"] = api_call_time(n)
@@ -1034,7 +1240,7 @@ def bench_single(args):
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_n)
         res["cpu_baseline_configs"] = cpu_baselines_configs()
-    print(json.dumps(res), flush=True)
+    print(fit_line(res, args.detail or default_detail(1)), flush=True)
 
 
 # --------------------------------------------------------------------------
@@ -1321,7 +1527,7 @@ def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200, 
     return out
 
 
-def start_watchdog(res, rank, deadline):
+def start_watchdog(res, rank, deadline, detail=None):
     """The N > 1 line's printer and deadline: emit() prints `res` once (rank
     0); if the run is still going after `deadline` seconds, the watchdog
     marks the line incomplete (naming state["phase"]), prints it and ends
@@ -1334,7 +1540,7 @@ def start_watchdog(res, rank, deadline):
         with printed:
             if rank == 0 and not state["printed"]:
                 state["printed"] = True
-                print(json.dumps(res), flush=True)
+                print(fit_line(res, detail), flush=True)
 
     def watchdog():
         time.sleep(deadline)
@@ -1404,7 +1610,8 @@ def bench_multi(args):
     res["launch"]["ranks"] = idents
     buses = [x.get("pci_bus_id") for x in idents]
     res["launch"]["distinct_gpus"] = None not in buses and len(set(buses)) == world
-    state, emit = start_watchdog(res, rank, args.deadline)
+    state, emit = start_watchdog(res, rank, args.deadline,
+                                 args.detail or default_detail(world))
 
     # ---- the device symmetric heap: ONE contiguous virtual range per PE
     # (osgpu_heap_create: dmabuf chunks mapped into every member), holding
