@@ -58,6 +58,7 @@ for sub in ("test-resilient-osss-ucx_amd", "oracle", "tests"):
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec, MI355X_MICROARCH.md
 XGMI_LINK_GBS = 76.8           # MI355X xGMI: 153.6 GB/s bidirectional per peer link
 GIB = float(1 << 30)
+HOST_FOLD_MAX_BYTES = 64 << 10  # runtime.cpp host_fold_max_bytes() default
 METRIC = "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2/4/8 GPU"
 
 
@@ -811,14 +812,11 @@ def team_placements(L, torch, n, reps, P, trials=3, canary=None):
     del arrs
     torch.cuda.empty_cache()
     med = sorted(runs, key=lambda r: r["frac_of_copy_ceiling"])[len(runs) // 2]
-    out = {k: med[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                               "traffic_source", "kernel", "members", "nreduce",
-                               "kernel_avg_us", "algorithmic_bytes_per_launch", "copy_frac",
-                               "frac_of_copy_ceiling")}
+    # (bound "hbm", peak 8000 GB/s, 2*P*nreduce*8 algorithmic bytes: the roofline's)
+    out = {k: med[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us", "traffic",
+                               "traffic_source", "copy_frac", "frac_of_copy_ceiling")}
     out["placements"] = runs      # full records (addresses): the detail file
     out["trials"] = [{"frac": r["frac"], "copy_frac": r["copy_frac"],
-                      "of_copy": r["frac_of_copy_ceiling"],
-                      "again_us": r["kernel_avg_us_again_after_copy"],
                       "canary": [r["canary_before"], r["canary_after"]]} for r in runs]
     for key, get in (("frac", lambda r: r["frac"]),
                      ("frac_of_copy_ceiling", lambda r: r["frac_of_copy_ceiling"])):
@@ -1018,14 +1016,15 @@ def small_call_latency(n=1024, reps=300, sizes=(1024, 4096, 8192, 16384, 32768, 
     lat = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["latency"]
     out = {"note": f"shmem_int_sum_to_all nreduce={n}, 2 PEs = 2 processes sharing this GPU, "
                    f"device-resident symmetric heaps, median of {reps} calls barrier to barrier"}
-    for k in ("fused_team", "team", "host_fused_staged", "host_staged"):
+    for k in ("fused_team", "team", "host_fused_staged", "host_staged", "host_fold"):
         v = lat[f"{n}/{k}"]
         out[k + "_us"] = v["us_median"]
         if "us_median_timed_in_c" in v:   # the loop in C, like the CPU baseline's
             out[k + "_us_timed_in_c"] = v["us_median_timed_in_c"]
         out[k + "_correct"] = v["correct"]
     out["note"] += ("; host_* = the same call on a pinned host symmetric heap (config 1's "
-                    "own placement): fused staged (one launch) vs pipelined STAGED")
+                    "own placement): fused staged (one launch) vs pipelined STAGED vs the "
+                    "host fold (the library's default up to 64 KiB per PE)")
     cpu = {}
     for m in sizes:
         src = O.team_inputs("int", 2, m, 5, "bits")
@@ -1034,8 +1033,14 @@ def small_call_latency(n=1024, reps=300, sizes=(1024, 4096, 8192, 16384, 32768, 
     out["cpu_reference_loop_us"] = cpu[n]
     sweep = [{"nreduce": m, "cpu_reference_loop_us": cpu[m],
               "fused_team_us": lat[f"{m}/fused_team"]["us_median"],
-              "host_fused_staged_us": lat[f"{m}/host_fused_staged"]["us_median"]}
+              "host_fused_staged_us": lat[f"{m}/host_fused_staged"]["us_median"],
+              "host_fold_us": lat[f"{m}/host_fold"].get("us_median_timed_in_c",
+                                                      lat[f"{m}/host_fold"]["us_median"]),
+              "host_fold_us_python": lat[f"{m}/host_fold"]["us_median"]}
              for m in sizes]
+    for rec in sweep:  # the library's default on a host heap at this size
+        rec["default_us"] = (rec["host_fold_us"] if rec["nreduce"] * 4 <= HOST_FOLD_MAX_BYTES
+                             else rec["host_fused_staged_us"])
     out["sweep"] = sweep
 
     def crossover(key):
@@ -1044,14 +1049,22 @@ def small_call_latency(n=1024, reps=300, sizes=(1024, 4096, 8192, 16384, 32768, 
             if all(x[key] < x["cpu_reference_loop_us"] for x in sweep[i:]):
                 return rec["nreduce"]
         return None
-    best = min(out["fused_team_us"], out["host_fused_staged_us"])
+    # config 1's placement is the host heap, whose default path at 1 Ki is
+    # the host fold: timed in C between the runtime's barriers, as the
+    # reference's loop is
+    dflt = out.get("host_fold_us_timed_in_c", out["host_fold_us"])
+    out["default_path_us"] = dflt
+    out["default_path"] = lat[f"{n}/host_fold"]["path"]
     out["crossover_elements"] = {"device_heaps_fused": crossover("fused_team_us"),
-                                 "pinned_host_heaps_fused": crossover("host_fused_staged_us")}
-    out["slower_than_reference_loop"] = best > cpu[n]
-    out["ratio_to_reference_loop"] = best / cpu[n]
-    out["crossover_note"] = ("below crossover_elements the drop-in's small call (kernel launch "
-                             "+ device barriers, >= ~11 us) is slower than the reference's CPU "
-                             "loop (kind: port, memcpy getmem, no UCX); from there on faster")
+                                 "pinned_host_heaps_fused": crossover("host_fused_staged_us"),
+                                 "pinned_host_heaps_default": crossover("default_us")}
+    out["slower_than_reference_loop"] = dflt > cpu[n]
+    out["ratio_to_reference_loop"] = dflt / cpu[n]
+    out["best_gpu_form_us"] = min(out["fused_team_us"], out["host_fused_staged_us"])
+    out["crossover_note"] = ("config 1 (1 Ki ints on host heaps): the default path is the host "
+                             "fold (one getmem per peer, direct fold); the GPU forms (kernel "
+                             "launch + device barriers, >= ~11 us) win from crossover_elements "
+                             "on (kind: port, memcpy getmem, no UCX)")
     return out
 
 
@@ -1418,15 +1431,8 @@ def _multi_fcollect(L, osgpu, torch, dist, rank, world, dev, hsrc, htgt, heap_by
     def steph():
         fc(ht.data_ptr(), hs.data_ptr(), nbh // 8, 0, 0, world, ps)
 
-    old = os.environ.get("OSGPU_HOST_PATH")
-    os.environ["OSGPU_HOST_PATH"] = "staged"
-    try:
+    with osgpu.host_path("staged"):
         t = _timed(steph, 3, 1, dist, torch)
-    finally:
-        if old is None:
-            os.environ.pop("OSGPU_HOST_PATH", None)
-        else:
-            os.environ["OSGPU_HOST_PATH"] = old
     out["host_staged_pinned"] = {"bytes_per_pe": nbh, "ms_per_call": t / 3 * 1e3,
                                  "GBps_per_pe": 3 * world * nbh / t / 1e9,
                                  "pcie_GBps_per_pe": 3 * (world + 1) * nbh / t / 1e9,

@@ -45,16 +45,15 @@ struct Inputs {
 
 constexpr int kBlock = 256;
 
-// above 6 inputs: vectors per input in flight per round (U = OSGPU_U_K8 in
-// all); G = U keeps every load of the tile in flight at once
-#ifndef OSGPU_COMBINE_G8
-#define OSGPU_COMBINE_G8 OSGPU_U_K8
-#endif
+// above 6 inputs: vectors per input in flight per round (U = kUK8 in all);
+// G = U keeps every load of the tile in flight at once (G = 2 and 1 were
+// measured no faster: tools/combine_variants.py)
+constexpr int kCombineG8 = kUK8;
 
 // lanes per vector-tile unroll: keep K*U*4 VGPRs of payload modest
 template <int K>
 struct Unroll {
-    static constexpr int value = K <= 2 ? OSGPU_U_K2 : (K <= 4 ? OSGPU_U_K4 : OSGPU_U_K8);
+    static constexpr int value = K <= 2 ? kUK2 : (K <= 4 ? kUK4 : kUK8);
 };
 
 template <typename T, int OP, int K>
@@ -120,9 +119,9 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
 
     if (tid + (size_t) (U - 1) * kBlock < nvec) {
         // the loads of G vectors of every input in flight before their folds
-        // (G = U: all K*U of them; above 6 inputs OSGPU_COMBINE_G8)
-        constexpr int G = K <= 6 ? U : OSGPU_COMBINE_G8;
-        static_assert(G >= 1 && G <= U && U % G == 0, "OSGPU_COMBINE_G8 must divide U");
+        // (G = U: all K*U of them; above 6 inputs kCombineG8)
+        constexpr int G = K <= 6 ? U : kCombineG8;
+        static_assert(G >= 1 && G <= U && U % G == 0, "kCombineG8 must divide U");
 #pragma unroll
         for (int g = 0; g < U; g += G) {
             Vec16<T> x[G][K];
@@ -153,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
     }
 }
 
-// LDS-staged form (OSGPU_COMBINE_LDS, 2 <= K <= OSGPU_COMBINE_LDS_MAX_K): K
+// LDS-staged form (2 <= K <= kCombineLdsMaxK): K
 // waves per workgroup, a tile of 64*U 16-B vectors of every input.  Wave k
 // streams input k's tile into LDS (one read stream per wave, like the copy
 // kernel and team_lds_kernel); after the barrier the K waves fold the tile
@@ -166,18 +165,11 @@ __global__ __launch_bounds__(kBlock) void combine_vec_kernel(
 // sum 1.02x / 1.04x, long xor 1.01x, double max 1.00x at K = 2; K = 5 and
 // 8 (32 Mi doubles) 1.04x and 1.07x with U = 4 (U = 2: 1.01x, 1.05x); at
 // 8 / 64 / 128 Mi doubles, K = 2: 1.07x / 1.04x / 1.04x.
-#ifndef OSGPU_COMBINE_LDS
-#define OSGPU_COMBINE_LDS 1
-#endif
-#ifndef OSGPU_COMBINE_LDS_MAX_K
-#define OSGPU_COMBINE_LDS_MAX_K 8
-#endif
+constexpr int kCombineLdsMaxK = 8;
 #ifndef OSGPU_COMBINE_LDS_U2
-#define OSGPU_COMBINE_LDS_U2 2  // vectors per lane per input at K = 2
+#define OSGPU_COMBINE_LDS_U2 2  // vectors per lane per input at K = 2 (the headline kernel)
 #endif
-#ifndef OSGPU_COMBINE_LDS_U
-#define OSGPU_COMBINE_LDS_U 4   // ... at K = 3 .. 8
-#endif
+constexpr int kCombineLdsU = 4;  // ... at K = 3 .. 8
 
 template <typename T, int OP, int K, int U>
 __global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K> in, size_t nvec,
@@ -255,8 +247,8 @@ static hipError_t launch_k(T *out, const T *const *srcs, size_t n, hipStream_t s
     size_t nvec = (n - head) / W;
     size_t tail_start = head + nvec * W;
     int nedge = (int) (head + (n - tail_start));
-    if constexpr (OSGPU_COMBINE_LDS && K >= 2 && K <= OSGPU_COMBINE_LDS_MAX_K) {
-        constexpr int UL = K == 2 ? OSGPU_COMBINE_LDS_U2 : OSGPU_COMBINE_LDS_U;
+    if constexpr (K >= 2 && K <= kCombineLdsMaxK) {
+        constexpr int UL = K == 2 ? OSGPU_COMBINE_LDS_U2 : kCombineLdsU;
         size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
         if (blocks == 0) blocks = 1;
         if (blocks > 0x7fffffffull) return hipErrorInvalidValue;

@@ -3,19 +3,12 @@
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
 
-// 16-byte vectors in flight per lane per input: for <= 2, <= 4 and <= 8
-// inputs (register budget vs bytes in flight; see tools/tune_combine.hip)
-#ifndef OSGPU_U_K2
-#define OSGPU_U_K2 4
-#endif
-#ifndef OSGPU_U_K4
-#define OSGPU_U_K4 4
-#endif
-#ifndef OSGPU_U_K8
-#define OSGPU_U_K8 4
-#endif
-
 namespace osgpu {
+
+// 16-byte vectors in flight per lane per input of the register-form combine
+// for <= 2, <= 4 and <= 8 inputs (register budget vs bytes in flight;
+// tools/tune_combine.hip)
+constexpr int kUK2 = 4, kUK4 = 4, kUK8 = 4;
 
 // type codes (same numbering as include/osgpu_reduce.h OSGPU_T_*)
 enum TypeCode {
@@ -33,9 +26,11 @@ hipError_t launch_combine(int type, int op, void *out, const void *const *srcs, 
 // for i < n, dsts[q][i] = fold of srcs[*][i] in PE q's order (q first, then
 // ascending, skipping q).  srcs/dsts indexed by position in the active set
 // and already offset to this PE's shard.
+// remote: some member's arrays live in another GPU's HBM (xGMI) -- the team
+// kernel then takes the shapes last measured across GPUs (team.hip TeamShape)
 constexpr int kMaxTeam = 8;
 hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
-                       size_t n, hipStream_t s);
+                       size_t n, hipStream_t s, bool remote = false);
 hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,
                                   size_t n, hipStream_t s);
 // The same over [0, n) split by tiles instead of contiguous shards: of m
@@ -44,7 +39,7 @@ hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *
 // same address range together (run_team).  m = 1, k = 0: launch_team.
 // hipErrorNotSupported for long double (contiguous shards only).
 hipError_t launch_team_tiles(int type, int op, int P, void *const *dsts, const void *const *srcs,
-                             size_t n, int m, int k, hipStream_t s);
+                             size_t n, int m, int k, hipStream_t s, bool remote = false);
 
 // Byte copy of up to kMaxCopySegs independent ranges in one launch (copy.hip):
 // the data movement of broadcast / collect / fcollect / alltoall.  Sources may
@@ -57,11 +52,16 @@ struct CopySeg {
     size_t bytes;
 };
 hipError_t launch_copy(const CopySeg *segs, int nseg, hipStream_t s);
+// Host fold of small host-heap calls (host_fold.hip): acc[i] = op(acc[i],
+// in[i]) for i < n with the kernels' element ops compiled for the host
+bool host_fold_supported(int type, int op);
+bool host_fold(int type, int op, void *acc, const void *in, size_t n);
 // One range between HBM and pinned host memory mapped into the GPU (either
 // side may be the host's device view): a fixed grid (OSGPU_HOST_COPY_GRID,
 // default 256 workgroups) sized for one PCIe link, not for HBM (copy.hip)
 hipError_t launch_host_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
-// <= 2 KiB of 8-byte words read with plain (L2-cached) loads into dst
+// <= kProbeLoadBytes of 8-byte words read with plain (L2-cached) loads into dst
+constexpr size_t kProbeLoadBytes = 2048;
 hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t s);
 
 // One-launch reduce-to-all for small calls (fused.hip): the call's two

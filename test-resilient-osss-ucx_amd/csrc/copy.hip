@@ -187,7 +187,8 @@ hipError_t launch_host_copy(void *dst, const void *src, size_t bytes, hipStream_
 
 hipError_t launch_probe_load(const void *src, void *dst, size_t bytes, hipStream_t stream)
 {
-    if (bytes % 8 || bytes / 8 > (size_t) kThreads || ((uintptr_t) src | (uintptr_t) dst) & 7)
+    static_assert(kProbeLoadBytes == (size_t) kThreads * 8, "one word per lane");
+    if (bytes % 8 || bytes > kProbeLoadBytes || ((uintptr_t) src | (uintptr_t) dst) & 7)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(probe_load_kernel, dim3(1), dim3(kThreads), 0, stream,
                        static_cast<const unsigned long long *>(src),

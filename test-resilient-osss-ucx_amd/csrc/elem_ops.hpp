@@ -23,50 +23,54 @@
 
 #pragma clang fp contract(off)
 
+// host + device: the kernels, and the host fold of small host-heap calls
+// (host_fold.hip) -- one definition of every element op for both
+#define OSGPU_EHD __host__ __device__ __forceinline__
+
 namespace osgpu {
 
 struct cfloat { float re, im; };
 struct cdouble { double re, im; };
 
 // ---------------------------------------------------------------- bit utils
-__device__ __forceinline__ uint64_t bits(double x) { return __double_as_longlong(x); }
-__device__ __forceinline__ double dbl(uint64_t u) { return __longlong_as_double((long long) u); }
-__device__ __forceinline__ uint32_t bits(float x) { return __float_as_uint(x); }
-__device__ __forceinline__ float flt(uint32_t u) { return __uint_as_float(u); }
+OSGPU_EHD uint64_t bits(double x) { return __builtin_bit_cast(uint64_t, x); }
+OSGPU_EHD double dbl(uint64_t u) { return __builtin_bit_cast(double, u); }
+OSGPU_EHD uint32_t bits(float x) { return __builtin_bit_cast(uint32_t, x); }
+OSGPU_EHD float flt(uint32_t u) { return __builtin_bit_cast(float, u); }
 
-__device__ __forceinline__ bool isnan_(double x) { return (bits(x) << 1) > (0x7ff0000000000000ull << 1); }
-__device__ __forceinline__ bool isnan_(float x) { return (bits(x) << 1) > (0x7f800000u << 1); }
-__device__ __forceinline__ bool isinf_(double x) { return (bits(x) << 1) == (0x7ff0000000000000ull << 1); }
-__device__ __forceinline__ bool isinf_(float x) { return (bits(x) << 1) == (0x7f800000u << 1); }
+OSGPU_EHD bool isnan_(double x) { return (bits(x) << 1) > (0x7ff0000000000000ull << 1); }
+OSGPU_EHD bool isnan_(float x) { return (bits(x) << 1) > (0x7f800000u << 1); }
+OSGPU_EHD bool isinf_(double x) { return (bits(x) << 1) == (0x7ff0000000000000ull << 1); }
+OSGPU_EHD bool isinf_(float x) { return (bits(x) << 1) == (0x7f800000u << 1); }
 
-__device__ __forceinline__ double quiet(double x) { return dbl(bits(x) | 0x0008000000000000ull); }
-__device__ __forceinline__ float quiet(float x) { return flt(bits(x) | 0x00400000u); }
-__device__ __forceinline__ double defnan(double) { return dbl(0xfff8000000000000ull); }
-__device__ __forceinline__ float defnan(float) { return flt(0xffc00000u); }
+OSGPU_EHD double quiet(double x) { return dbl(bits(x) | 0x0008000000000000ull); }
+OSGPU_EHD float quiet(float x) { return flt(bits(x) | 0x00400000u); }
+OSGPU_EHD double defnan(double) { return dbl(0xfff8000000000000ull); }
+OSGPU_EHD float defnan(float) { return flt(0xffc00000u); }
 
 // SSE NaN selection for `r = a OP b` with first source a.  The branch is
 // taken only when r is NaN, so the streaming fast path pays one compare.
 template <typename F>
-__device__ __forceinline__ F sse(F r, F a, F b)
+OSGPU_EHD F sse(F r, F a, F b)
 {
     if (__builtin_expect(r != r, 0)) {
         r = isnan_(a) ? quiet(a) : (isnan_(b) ? quiet(b) : defnan(a));
     }
     return r;
 }
-template <typename F> __device__ __forceinline__ F add(F a, F b) { return sse<F>(a + b, a, b); }
-template <typename F> __device__ __forceinline__ F sub(F a, F b) { return sse<F>(a - b, a, b); }
-template <typename F> __device__ __forceinline__ F mul(F a, F b) { return sse<F>(a * b, a, b); }
+template <typename F> OSGPU_EHD F add(F a, F b) { return sse<F>(a + b, a, b); }
+template <typename F> OSGPU_EHD F sub(F a, F b) { return sse<F>(a - b, a, b); }
+template <typename F> OSGPU_EHD F mul(F a, F b) { return sse<F>(a * b, a, b); }
 
 template <typename F>
-__device__ __forceinline__ F copysign_(F mag, F sgn);
+OSGPU_EHD F copysign_(F mag, F sgn);
 template <>
-__device__ __forceinline__ double copysign_(double m, double s)
+OSGPU_EHD double copysign_(double m, double s)
 {
     return dbl((bits(m) & 0x7fffffffffffffffull) | (bits(s) & 0x8000000000000000ull));
 }
 template <>
-__device__ __forceinline__ float copysign_(float m, float s)
+OSGPU_EHD float copysign_(float m, float s)
 {
     return flt((bits(m) & 0x7fffffffu) | (bits(s) & 0x80000000u));
 }
@@ -81,7 +85,7 @@ struct CPair {
 };
 // returned by value (in registers): no stack frame on the fast path's kernels
 template <typename F>
-__device__ __attribute__((noinline)) CPair<F> mulc3(F a, F b, F c, F d)
+__host__ __device__ __attribute__((noinline)) CPair<F> mulc3(F a, F b, F c, F d)
 {
     const F one = 1, zero = 0, inf = __builtin_huge_val();
     F ac = mul(a, c), bd = mul(b, d), ad = mul(a, d), bc = mul(c, b);
@@ -133,49 +137,49 @@ template <typename T, int OP> struct Elem;
 
 // integers ---------------------------------------------------------------
 template <typename T> struct Elem<T, OP_SUM> {
-    __device__ __forceinline__ static T f(T a, T b)
+    OSGPU_EHD static T f(T a, T b)
     {
         using U = typename Unsigned<T>::type;
         return (T) (U) ((U) a + (U) b);
     }
 };
 template <typename T> struct Elem<T, OP_PROD> {
-    __device__ __forceinline__ static T f(T a, T b)
+    OSGPU_EHD static T f(T a, T b)
     {
         using U = typename Unsigned<T>::type;
         return (T) (U) ((U) a * (U) b);
     }
 };
-template <typename T> struct Elem<T, OP_AND> { __device__ __forceinline__ static T f(T a, T b) { return a & b; } };
-template <typename T> struct Elem<T, OP_OR> { __device__ __forceinline__ static T f(T a, T b) { return a | b; } };
-template <typename T> struct Elem<T, OP_XOR> { __device__ __forceinline__ static T f(T a, T b) { return a ^ b; } };
+template <typename T> struct Elem<T, OP_AND> { OSGPU_EHD static T f(T a, T b) { return a & b; } };
+template <typename T> struct Elem<T, OP_OR> { OSGPU_EHD static T f(T a, T b) { return a | b; } };
+template <typename T> struct Elem<T, OP_XOR> { OSGPU_EHD static T f(T a, T b) { return a ^ b; } };
 // compare + select: exact for every type, including NaN / signed zero
-template <typename T> struct Elem<T, OP_MAX> { __device__ __forceinline__ static T f(T a, T b) { return a > b ? a : b; } };
-template <typename T> struct Elem<T, OP_MIN> { __device__ __forceinline__ static T f(T a, T b) { return a < b ? a : b; } };
+template <typename T> struct Elem<T, OP_MAX> { OSGPU_EHD static T f(T a, T b) { return a > b ? a : b; } };
+template <typename T> struct Elem<T, OP_MIN> { OSGPU_EHD static T f(T a, T b) { return a < b ? a : b; } };
 
 // real floating point ------------------------------------------------------
-template <> struct Elem<float, OP_SUM> { __device__ __forceinline__ static float f(float a, float b) { return add(a, b); } };
-template <> struct Elem<float, OP_PROD> { __device__ __forceinline__ static float f(float a, float b) { return mul(a, b); } };
-template <> struct Elem<double, OP_SUM> { __device__ __forceinline__ static double f(double a, double b) { return add(a, b); } };
-template <> struct Elem<double, OP_PROD> { __device__ __forceinline__ static double f(double a, double b) { return mul(a, b); } };
+template <> struct Elem<float, OP_SUM> { OSGPU_EHD static float f(float a, float b) { return add(a, b); } };
+template <> struct Elem<float, OP_PROD> { OSGPU_EHD static float f(float a, float b) { return mul(a, b); } };
+template <> struct Elem<double, OP_SUM> { OSGPU_EHD static double f(double a, double b) { return add(a, b); } };
+template <> struct Elem<double, OP_PROD> { OSGPU_EHD static double f(double a, double b) { return mul(a, b); } };
 
 // complex ----------------------------------------------------------------
 // complexd sum: compiled as addsd %xmm3,%xmm1 ; addsd %xmm2,%xmm0 (a first)
 template <> struct Elem<cdouble, OP_SUM> {
-    __device__ __forceinline__ static cdouble f(cdouble a, cdouble b)
+    OSGPU_EHD static cdouble f(cdouble a, cdouble b)
     {
         return cdouble{add(a.re, b.re), add(a.im, b.im)};
     }
 };
 // complexf sum: the compiled body adds the imaginary parts as b.im + a.im
 template <> struct Elem<cfloat, OP_SUM> {
-    __device__ __forceinline__ static cfloat f(cfloat a, cfloat b)
+    OSGPU_EHD static cfloat f(cfloat a, cfloat b)
     {
         return cfloat{add(a.re, b.re), add(b.im, a.im)};
     }
 };
 template <typename C, typename F>
-__device__ __forceinline__ C cmul(C p, C q)
+OSGPU_EHD C cmul(C p, C q)
 {
     F a = p.re, b = p.im, c = q.re, d = q.im;
     F x = a * c - b * d;   // inline fast path; any NaN part -> libgcc path
@@ -188,10 +192,10 @@ __device__ __forceinline__ C cmul(C p, C q)
     return C{x, y};
 }
 template <> struct Elem<cdouble, OP_PROD> {
-    __device__ __forceinline__ static cdouble f(cdouble a, cdouble b) { return cmul<cdouble, double>(a, b); }
+    OSGPU_EHD static cdouble f(cdouble a, cdouble b) { return cmul<cdouble, double>(a, b); }
 };
 template <> struct Elem<cfloat, OP_PROD> {
-    __device__ __forceinline__ static cfloat f(cfloat a, cfloat b) { return cmul<cfloat, float>(a, b); }
+    OSGPU_EHD static cfloat f(cfloat a, cfloat b) { return cmul<cfloat, float>(a, b); }
 };
 
 // ------------------------------------------------------- branch-free folds
@@ -208,13 +212,13 @@ template <> struct Elem<cfloat, OP_PROD> {
 // kChecked = false and the test compiles away.
 template <typename T, int OP> struct Fast {
     static constexpr bool kChecked = false;
-    __device__ __forceinline__ static T f(T a, T b) { return Elem<T, OP>::f(a, b); }
-    __device__ __forceinline__ static bool bad(T) { return false; }
+    OSGPU_EHD static T f(T a, T b) { return Elem<T, OP>::f(a, b); }
+    OSGPU_EHD static bool bad(T) { return false; }
 };
 template <typename F, int OP> struct FastReal {
     static constexpr bool kChecked = true;
-    __device__ __forceinline__ static F f(F a, F b) { return OP == OP_SUM ? a + b : a * b; }
-    __device__ __forceinline__ static bool bad(F r) { return r != r; }
+    OSGPU_EHD static F f(F a, F b) { return OP == OP_SUM ? a + b : a * b; }
+    OSGPU_EHD static bool bad(F r) { return r != r; }
 };
 template <> struct Fast<float, OP_SUM> : FastReal<float, OP_SUM> {};
 template <> struct Fast<float, OP_PROD> : FastReal<float, OP_PROD> {};
@@ -222,27 +226,27 @@ template <> struct Fast<double, OP_SUM> : FastReal<double, OP_SUM> {};
 template <> struct Fast<double, OP_PROD> : FastReal<double, OP_PROD> {};
 template <> struct Fast<cdouble, OP_SUM> {
     static constexpr bool kChecked = true;
-    __device__ __forceinline__ static cdouble f(cdouble a, cdouble b)
+    OSGPU_EHD static cdouble f(cdouble a, cdouble b)
     {
         return cdouble{a.re + b.re, a.im + b.im};
     }
-    __device__ __forceinline__ static bool bad(cdouble r) { return r.re != r.re || r.im != r.im; }
+    OSGPU_EHD static bool bad(cdouble r) { return r.re != r.re || r.im != r.im; }
 };
 template <> struct Fast<cfloat, OP_SUM> {
     static constexpr bool kChecked = true;
-    __device__ __forceinline__ static cfloat f(cfloat a, cfloat b)
+    OSGPU_EHD static cfloat f(cfloat a, cfloat b)
     {
         return cfloat{a.re + b.re, b.im + a.im};  // the compiled order, as Elem
     }
-    __device__ __forceinline__ static bool bad(cfloat r) { return r.re != r.re || r.im != r.im; }
+    OSGPU_EHD static bool bad(cfloat r) { return r.re != r.re || r.im != r.im; }
 };
 template <typename C, typename F> struct FastCplxProd {
     static constexpr bool kChecked = true;
-    __device__ __forceinline__ static C f(C p, C q)
+    OSGPU_EHD static C f(C p, C q)
     {
         return C{p.re * q.re - p.im * q.im, p.re * q.im + p.im * q.re};  // cmul's inline form
     }
-    __device__ __forceinline__ static bool bad(C r) { return r.re != r.re || r.im != r.im; }
+    OSGPU_EHD static bool bad(C r) { return r.re != r.re || r.im != r.im; }
 };
 template <> struct Fast<cdouble, OP_PROD> : FastCplxProd<cdouble, double> {};
 template <> struct Fast<cfloat, OP_PROD> : FastCplxProd<cfloat, float> {};

@@ -73,6 +73,7 @@ struct Heap {                        // the heap a PE created, with its imports
     std::vector<int> members;
     std::vector<char *> member_base; // every member's range as seen here, by set index
     std::vector<size_t> member_bytes;
+    std::vector<char> member_remote; // backed by another GPU's HBM (reached over xGMI)
     Mapping own;
     std::vector<Mapping> peers;      // members in other processes
 };
@@ -88,7 +89,7 @@ std::vector<Heap *> g_pool;
 
 // what a PE publishes in pSync[16..] during osgpu_heap_create
 struct HeapMsg {
-    long pid, nonce, bytes, chunk, raw_ptr, status, device, seg;
+    long pid, nonce, bytes, chunk, raw_ptr, status, device, seg, pci;
 };
 static_assert(sizeof(HeapMsg) <= (64 - kHeapPsync) * sizeof(long), "pSync room");
 
@@ -264,11 +265,12 @@ bool map_chunks(Mapping &m, size_t align, int dev)
 
 size_t heap_chunk_bytes(size_t gran)
 {
-    const char *e = getenv("OSGPU_HEAP_CHUNK_BYTES");
-    size_t c = e ? strtoull(e, nullptr, 0) : 0;
-    if (!c) c = (size_t) 1 << 30;
-    c = (c + gran - 1) / gran * gran;
-    return c;
+    static const size_t env = [] {  // read once
+        const char *e = getenv("OSGPU_HEAP_CHUNK_BYTES");
+        const size_t v = e ? strtoull(e, nullptr, 0) : 0;
+        return v ? v : (size_t) 1 << 30;
+    }();
+    return (env + gran - 1) / gran * gran;
 }
 
 }  // namespace
@@ -381,9 +383,11 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
             cand->seg = rseg;
             g_heaps.push_back(cand);
         }
-        for (int i = 0; i < PE_size; i++)  // cannot fail: arguments checked above
+        for (int i = 0; i < PE_size; i++) {  // cannot fail: arguments checked above
             (void) osgpu_heap_register_segment(c.pe_at(i), rseg, cand->member_base[i],
                                                std::min(total, cand->member_bytes[i]));
+            heap_set_remote(c.pe_at(i), rseg, cand->member_remote[i] != 0);
+        }
         delete H;
         *base_out = cand->own.base;
         DBG("%s PE %d: kept heap %p of %zu B registered again for %zu B (segment %d)", where,
@@ -464,6 +468,7 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
     mine->chunk = (long) chunk;
     mine->raw_ptr = (long) (uintptr_t) H->own.base;
     mine->device = dev;
+    mine->pci = pci_key(dev);
     // every heap of a member set gets its own registry segment: the lowest
     // one free for every member here, agreed as the maximum over members
     mine->seg = heap_free_segment(H->members);
@@ -658,10 +663,16 @@ extern "C" int osgpu_heap_create(size_t bytes, int PE_start, int logPE_stride, i
         if (ok) set_err("%s: another member failed to create or map its heap", where);
         return OSGPU_EPEER;
     }
+    int me_idx = 0;
+    for (int i = 0; i < PE_size; i++)
+        if (c.pe_at(i) == c.me) me_idx = i;
     unsigned long long key = 0x9e3779b97f4a7c15ull;  // the same on every member
     for (int i = 0; i < PE_size; i++) {
         // cannot fail: base and size checked, segment within the registry
         (void) osgpu_heap_register_segment(c.pe_at(i), H->seg, base[i], (size_t) msg[i].bytes);
+        const bool remote = msg[i].pci != msg[me_idx].pci;
+        heap_set_remote(c.pe_at(i), H->seg, remote);
+        H->member_remote.push_back(remote ? 1 : 0);
         H->member_base.push_back(base[i]);
         H->member_bytes.push_back((size_t) msg[i].bytes);
         key = (key ^ (unsigned long long) msg[i].pid) * 0x100000001b3ull;
@@ -971,9 +982,15 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
                  b.end ? "high" : "low", what);
         write_bad[i] += m;
     };
-    // the owner's view of its blocks, read by kernel with cached loads
+    // the owner's view of its blocks, read by kernel with cached loads, in
+    // pieces of at most kProbeLoadBytes (one probe workgroup: a block of a
+    // set of more than 128 members is larger)
     auto owner_read = [&](const WBlock &b, unsigned long long *got) {
-        hipError_t e = have_wtmp ? osgpu::launch_probe_load(b.at, wtmp, WB, st) : hipErrorOutOfMemory;
+        hipError_t e = have_wtmp ? hipSuccess : hipErrorOutOfMemory;
+        for (size_t o = 0; e == hipSuccess && o < WB; o += osgpu::kProbeLoadBytes) {
+            const size_t len = WB - o < osgpu::kProbeLoadBytes ? WB - o : osgpu::kProbeLoadBytes;
+            e = osgpu::launch_probe_load(b.at + o, wtmp + o, len, st);
+        }
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e == hipSuccess) e = hipMemcpy(got, wtmp, WB, hipMemcpyDeviceToHost);
         (void) hipGetLastError();
@@ -1079,8 +1096,16 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
 // osgpu_preflight calls of this process -- PE `pe` reaches peer `peer`
 // through another member's ranges.  (-1, -1) clears it.  Logged, so a
 // planted fault never goes unseen.
+// Not in the public header (tests/support/osgpu_test_hooks.h) and refused
+// unless the process runs with OSGPU_TEST_HOOKS=1: a production caller can
+// never redirect preflight writes by accident.
 extern "C" int osgpu_test_preflight_fault(int pe, int peer)
 {
+    const char *on = getenv("OSGPU_TEST_HOOKS");
+    if (!on || strcmp(on, "1")) {
+        set_err("osgpu_test_preflight_fault: test hooks are off (OSGPU_TEST_HOOKS=1 enables them)");
+        return OSGPU_EINVAL;
+    }
     if ((pe < 0) != (peer < 0)) return OSGPU_EINVAL;
     g_fault_pe.store(-1);
     g_fault_peer.store(peer);

@@ -72,16 +72,14 @@ struct LdVecInputs {
 };
 
 // elements in flight per lane for 3..8 inputs (soft-float registers)
-#ifndef OSGPU_LD_U_K8
-#define OSGPU_LD_U_K8 4
-#endif
+constexpr int kLdUK8 = 4;
 
 // 16-byte aligned arrays: one dwordx4 per element per input, U elements per
 // lane with every load issued before the soft-float fold
 template <int OP, int K>
 __global__ __launch_bounds__(256) void ld_vec_kernel(u64x2 *out, LdVecInputs<K> in, size_t n)
 {
-    constexpr int U = K <= 2 ? 4 : OSGPU_LD_U_K8;
+    constexpr int U = K <= 2 ? 4 : kLdUK8;
     const size_t base = (size_t) blockIdx.x * (256 * U) + threadIdx.x;
     u64x2 raw[U][K];
 #pragma unroll
@@ -112,7 +110,7 @@ static hipError_t ld_vec_launch(int K, void *out, const void *const *srcs, size_
     case KK: {                                                                 \
         LdVecInputs<KK> in;                                                    \
         for (int k = 0; k < KK; k++) in.p[k] = (const u64x2 *) srcs[k];        \
-        constexpr int U = KK <= 2 ? 4 : OSGPU_LD_U_K8;                                     \
+        constexpr int U = KK <= 2 ? 4 : kLdUK8;                                     \
         size_t blocks = (n + 256 * U - 1) / (256 * U);                         \
         hipLaunchKernelGGL((ld_vec_kernel<OP, KK>), dim3((unsigned) (blocks ? blocks : 1)), \
                            dim3(256), 0, s, (u64x2 *) out, in, n);             \

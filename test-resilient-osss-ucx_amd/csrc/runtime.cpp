@@ -69,6 +69,22 @@ int debug_level()
     return lvl;
 }
 
+// Environment knobs are read ONCE each (function-local statics at their
+// points of use), never per call; include/osgpu_reduce.h lists them.
+static long long env_ll(const char *var, long long def)
+{
+    const char *e = getenv(var);
+    return e && *e ? strtoll(e, nullptr, 0) : def;
+}
+
+static int env_word(const char *var, const char *const *words, int n, int def)
+{
+    const char *e = getenv(var);
+    for (int i = 0; e && i < n; i++)
+        if (!strcmp(e, words[i])) return i;
+    return def;
+}
+
 // ----------------------------------------------------------- synchronisation
 
 int env_choice(const char *var, const char *alt, int def_is_alt)
@@ -354,12 +370,20 @@ bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off)
 }
 
 // address of the symmetric object at (seg, off) on PE pe, checked for nbytes
-bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out)
+bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out, bool *remote)
 {
     HeapEntry h;
     if (!heap_segment(pe, seg, &h) || off + nbytes > h.bytes) return false;
     *out = h.base + off;
+    if (remote) *remote = h.remote;
     return true;
+}
+
+void heap_set_remote(int pe, int seg, bool remote)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (pe >= 0 && (size_t) pe < g_heap.size() && seg >= 0 && (size_t) seg < g_heap[pe].size())
+        g_heap[pe][seg].remote = remote;
 }
 
 // lowest segment index free on every PE of `pes` in this process's registry
@@ -633,12 +657,20 @@ constexpr int kPsyncBase = 16;  // pSync[16..28] used during setup only
 
 std::map<std::tuple<int, int, int, int, int>, StageSet> g_stage;  // (me, set, device)
 
+long long g_stage_bytes = -1;  // osgpu_set_stage_bytes; -1: OSGPU_STAGE_BYTES, 32 MiB
+
 size_t stage_slot_bytes()
 {
-    const char *e = getenv("OSGPU_STAGE_BYTES");
-    size_t b = e ? strtoull(e, nullptr, 0) : 0;
-    b = b ? b : (size_t) 32 << 20;
-    return (b + 255) & ~(size_t) 255;
+    static const long long env = [] {
+        const long long v = env_ll("OSGPU_STAGE_BYTES", 0);
+        return v > 0 ? v : (32LL << 20);
+    }();
+    long long b;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        b = g_stage_bytes > 0 ? g_stage_bytes : env;
+    }
+    return ((size_t) b + 255) & ~(size_t) 255;
 }
 
 struct StageMsg {  // what a PE publishes in pSync[16..30]
@@ -648,7 +680,6 @@ struct StageMsg {  // what a PE publishes in pSync[16..30]
 // the smallest pSync a caller hands us: SHMEM_BCAST/COLLECT/ALLTOALL_SYNC_SIZE
 static_assert(sizeof(StageMsg) <= (64 - kPsyncBase) * sizeof(long), "pSync room");
 
-// PCI location of a device: PEs with equal keys share one GPU and its link
 long pci_key(int dev)
 {
     int dom = 0, bus = 0, d = 0;
@@ -767,9 +798,12 @@ extern "C" int osgpu_copy_stream_priorities(int least, int greatest, int *in, in
 
 static void create_copy_stream(const char *where, int dev, hipStream_t *s, bool out)
 {
-    const char *e = getenv("OSGPU_COPY_STREAMS");
-    const bool plain = e && !strcmp(e, "plain");
-    bool cumask = e && !strcmp(e, "cumask");
+    static const int mode = [] {
+        static const char *w[] = {"prio", "plain", "cumask"};
+        return env_word("OSGPU_COPY_STREAMS", w, 3, 0);
+    }();
+    const bool plain = mode == 1;
+    bool cumask = mode == 2;
     if (!plain && !cumask) {
         int least = 0, greatest = 0, pin = 0, pout = 0;
         HIPCHK(where, hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -872,29 +906,88 @@ void *host_device_view(const void *p, size_t nbytes)
     return nullptr;
 }
 
-int g_team_exchange = -1;  // -1: from OSGPU_TEAM_EXCHANGE (pull|push), default pull
+// Settings with a setter (osgpu_set_*) and an environment default (env_ll /
+// env_word, read once into a function-local static the first time a setting
+// is needed); a setter's value wins until it is set back to -1.
+int g_team_exchange = -1;  // -1: OSGPU_TEAM_EXCHANGE (pull|push), default pull
 
 int team_exchange()
 {
+    static const int env = [] {
+        static const char *w[] = {"pull", "push"};
+        return env_word("OSGPU_TEAM_EXCHANGE", w, 2, 0);
+    }();
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_team_exchange < 0) {
-        const char *e = getenv("OSGPU_TEAM_EXCHANGE");
-        g_team_exchange = (e && !strcmp(e, "push")) ? 1 : 0;
-    }
-    return g_team_exchange;
+    return g_team_exchange < 0 ? env : g_team_exchange;
 }
 
-long long g_fused_max = -1;  // -1: from the environment
+long long g_fused_max = -1;  // -1: OSGPU_FUSED_MAX_BYTES, default 1 MiB
 
 size_t fused_max_bytes()
 {
+    static const long long env = [] {
+        const long long v = env_ll("OSGPU_FUSED_MAX_BYTES", 1LL << 20);
+        return v < 0 ? 0 : v;
+    }();
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_fused_max < 0) {
-        const char *e = getenv("OSGPU_FUSED_MAX_BYTES");
-        g_fused_max = e ? strtoll(e, nullptr, 0) : (1LL << 20);
-        if (g_fused_max < 0) g_fused_max = 0;
-    }
-    return (size_t) g_fused_max;
+    return (size_t) (g_fused_max < 0 ? env : g_fused_max);
+}
+
+// Host symmetric-heap calls (shmem_reduce.cpp to_all, shmem_collect.cpp):
+// OSGPU_HOST_PATH = auto | staged | getmem (osgpu_set_host_path).
+int g_host_path = -1;
+
+int host_path()
+{
+    static const int env = [] {
+        static const char *w[] = {"auto", "staged", "getmem"};
+        return env_word("OSGPU_HOST_PATH", w, 3, OSGPU_HOST_AUTO);
+    }();
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_host_path < 0 ? env : g_host_path;
+}
+
+// Per-PE byte limit of the host fold (host_fold.hip) on the automatic host
+// path: OSGPU_HOST_FOLD_MAX_BYTES, default 64 KiB (16 Ki ints; the measured
+// crossovers: DESIGN.md 10); 0 turns it off.
+long long g_host_fold_max = -1;
+
+size_t host_fold_max_bytes()
+{
+    static const long long env = [] {
+        const long long v = env_ll("OSGPU_HOST_FOLD_MAX_BYTES", 64LL << 10);
+        return v < 0 ? 0 : v;
+    }();
+    std::lock_guard<std::mutex> lk(g_mu);
+    return (size_t) (g_host_fold_max < 0 ? env : g_host_fold_max);
+}
+
+// How the STAGED path's legs cross PCIe: OSGPU_STAGE_COPY = dma | kout |
+// kernel (osgpu_set_stage_copy; shmem_reduce.cpp stage_leg).
+int g_stage_copy = -1;
+
+int stage_copy_mode()
+{
+    static const int env = [] {
+        static const char *w[] = {"dma", "kout", "kernel"};
+        return env_word("OSGPU_STAGE_COPY", w, 3, 0);
+    }();
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_stage_copy < 0 ? env : g_stage_copy;
+}
+
+// Chunk of the GETMEM host path: OSGPU_HOST_CHUNK_BYTES, default 64 MiB
+// (osgpu_set_host_chunk_bytes).
+long long g_host_chunk = -1;
+
+size_t host_chunk_bytes()
+{
+    static const long long env = [] {
+        const long long v = env_ll("OSGPU_HOST_CHUNK_BYTES", 0);
+        return v > 0 ? v : (64LL << 20);
+    }();
+    std::lock_guard<std::mutex> lk(g_mu);
+    return (size_t) (g_host_chunk <= 0 ? env : g_host_chunk);
 }
 
 // ---------------------------------------------------------------------
@@ -934,15 +1027,16 @@ int g_dbar_fatal = 1;
 
 static double fused_bound_secs()
 {
+    static const double env = [] {
+        const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
+        return e ? atof(e) : 0.0;
+    }();
     double secs;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         secs = g_dbar_secs;
     }
-    if (secs <= 0) {
-        const char *e = getenv("OSGPU_DEVICE_BARRIER_TIMEOUT_S");
-        secs = e ? atof(e) : 0.0;
-    }
+    if (secs <= 0) secs = env;
     return secs > 0 ? secs : 0.0;
 }
 
@@ -1122,6 +1216,7 @@ int osgpu_heap_register_segment(int pe, int seg, void *base, size_t bytes)
     if ((size_t) seg >= g_heap[pe].size()) g_heap[pe].resize(seg + 1);
     g_heap[pe][seg].base = (char *) base;
     g_heap[pe][seg].bytes = bytes;
+    g_heap[pe][seg].remote = false;  // caller-made segments: the local shapes
     return OSGPU_OK;
 }
 
@@ -1355,6 +1450,43 @@ int osgpu_set_fused_max_bytes(long long bytes)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     g_fused_max = bytes < 0 ? -1 : bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_set_host_path(int mode)
+{
+    if (mode < -1 || mode > OSGPU_HOST_GETMEM) return OSGPU_EINVAL;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_host_path = mode;
+    return OSGPU_OK;
+}
+
+int osgpu_set_host_fold_max_bytes(long long bytes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_host_fold_max = bytes < 0 ? -1 : bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_set_stage_copy(int mode)
+{
+    if (mode < -1 || mode > 2) return OSGPU_EINVAL;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_stage_copy = mode;
+    return OSGPU_OK;
+}
+
+int osgpu_set_stage_bytes(long long bytes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_stage_bytes = bytes <= 0 ? -1 : bytes;
+    return OSGPU_OK;
+}
+
+int osgpu_set_host_chunk_bytes(long long bytes)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_host_chunk = bytes <= 0 ? -1 : bytes;
     return OSGPU_OK;
 }
 

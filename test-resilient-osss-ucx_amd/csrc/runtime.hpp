@@ -75,10 +75,14 @@ PeOps pe_ops();
 struct HeapEntry {
     char *base = nullptr;
     size_t bytes = 0;
+    bool remote = false;  // backed by another GPU's HBM (osgpu_heap_create knows)
 };
 bool heap_segment(int pe, int seg, HeapEntry *out);
 bool heap_locate(int pe, const void *addr, size_t nbytes, int *seg, size_t *off);
-bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out);
+bool heap_peer(int pe, int seg, size_t off, size_t nbytes, char **out, bool *remote = nullptr);
+void heap_set_remote(int pe, int seg, bool remote);
+// PCI location of a device: PEs with equal keys share one GPU and its link
+long pci_key(int dev);
 // [p, p + n) inside a heap made by osgpu_heap_create (heap.cpp) -- the PE's
 // own range (*dev = its device) or a member's mapped here (*dev = -1)
 bool heap_created_range(const void *p, size_t n, int *dev);
@@ -210,6 +214,13 @@ void *host_device_view(const void *p, size_t nbytes);
 // Per-PE byte limit of the fused path: osgpu_set_fused_max_bytes, else
 // OSGPU_FUSED_MAX_BYTES, else 1 MiB; 0 = fused path off.
 size_t fused_max_bytes();
+// host symmetric-heap calls: OSGPU_HOST_AUTO / _STAGED / _GETMEM
+// (osgpu_set_host_path), the host fold's per-PE limit, the STAGED legs'
+// copy mode (0 dma, 1 kout, 2 kernel) and the GETMEM path's chunk
+int host_path();
+size_t host_fold_max_bytes();
+int stage_copy_mode();
+size_t host_chunk_bytes();
 
 }  // namespace rt
 }  // namespace osgpu

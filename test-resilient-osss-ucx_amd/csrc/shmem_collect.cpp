@@ -585,11 +585,12 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
         // shares) stay on the runtime's getmem: no GPU round trip beats a
         // same-node copy of a few KiB (1 Ki ints: 1.6 us vs 14 us for the
         // one-launch staged form, profiles/r01_mp_latency_host_coll.jsonl).
-        // OSGPU_HOST_PATH=staged|getmem overrides; forced staging runs small
-        // calls as one launch (run_fused_staged_copy).
-        const char *hp = getenv("OSGPU_HOST_PATH");
-        const bool force_getmem = hp && !strcmp(hp, "getmem");
-        const bool force_staged = hp && !strcmp(hp, "staged");
+        // osgpu_set_host_path / OSGPU_HOST_PATH=staged|getmem override;
+        // forced staging runs small calls as one launch
+        // (run_fused_staged_copy).
+        const int hp = host_path();
+        const bool force_getmem = hp == OSGPU_HOST_GETMEM;
+        const bool force_staged = hp == OSGPU_HOST_STAGED;
         StageSet *S = force_getmem ? nullptr : stage_setup(c);
         if (S && force_staged && !counts_done && run_fused_staged_copy(c, *S)) return;
         if (!counts_done) barrier(c);  // sources ready

@@ -91,7 +91,8 @@ bool member_sources(const Call &c, std::vector<const void *> &srcs)
 // every active PE's registered heap at the same offsets (symmetric), no
 // overlap between them, and 2 <= PE_size <= 8.  Fills srcs/dsts in active-set
 // order and returns this PE's index, or -1.
-int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *> &dsts)
+int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *> &dsts,
+              bool *remote = nullptr)
 {
     if (c.PE_size < 2 || c.PE_size > osgpu::kMaxTeam) return -1;
     if (ranges_overlap(c.target, c.source, c.nbytes)) return -1;
@@ -102,14 +103,18 @@ int team_ptrs(const Call &c, std::vector<const void *> &srcs, std::vector<void *
     srcs.resize(c.PE_size);
     dsts.resize(c.PE_size);
     int idx = -1;
+    bool far = false;
     for (int i = 0, pe = c.PE_start; i < c.PE_size; i++, pe += c.step) {
         char *sp = nullptr, *tp = nullptr;
-        if (!heap_peer(pe, ss, os, c.nbytes, &sp) || !heap_peer(pe, st, ot, c.nbytes, &tp))
+        bool rs = false, rt_ = false;
+        if (!heap_peer(pe, ss, os, c.nbytes, &sp, &rs) || !heap_peer(pe, st, ot, c.nbytes, &tp, &rt_))
             return -1;
         srcs[i] = sp;
         dsts[i] = tp;
+        far = far || rs || rt_;
         if (pe == c.me) idx = i;
     }
+    if (remote) *remote = far;
     return idx;
 }
 
@@ -153,7 +158,7 @@ int local_mode()
 }
 
 void run_team(const Call &c, const std::vector<const void *> &srcs,
-              const std::vector<void *> &dsts, int idx)
+              const std::vector<void *> &dsts, int idx, bool remote)
 {
     hipStream_t st = pe_stream(c.name, c.me);
     const size_t s = type_size(c.type);
@@ -209,7 +214,7 @@ void run_team(const Call &c, const std::vector<const void *> &srcs,
     }
     if (hi > lo) {
         hipError_t e = osgpu::launch_team_tiles(c.type, c.op, c.PE_size, dp.data(), sp.data(),
-                                                (size_t) (hi - lo), m, k, st);
+                                                (size_t) (hi - lo), m, k, st, remote);
         if (e != hipSuccess) fatal(c.name, "team combine launch: %s", hipGetErrorString(e));
     }
     call_trace(c.me, 3, "launch");
@@ -289,7 +294,7 @@ void run_team_push(const Call &c, const std::vector<const void *> &srcs,
                 dp[i] = (char *) dsts[i] + (size_t) a * s;
             }
             hipError_t e = osgpu::launch_team(c.type, c.op, P, dp.data(), sp.data(),
-                                              (size_t) (b - a), st);
+                                              (size_t) (b - a), st, S.ndev > 1);
             if (e != hipSuccess) fatal(c.name, "team fold launch: %s", hipGetErrorString(e));
             stream_wait(c.name, st);
         }
@@ -505,14 +510,8 @@ void run_rccl(const Call &c)
 //   hold 54 (tools/d2h_timeline.hip, profiles/r05_dma_state_timeline.jsonl);
 //   the bench reports that state beside the rates (dma_state).
 // A leg whose host memory has no device view takes the DMA engine.
+// (runtime.cpp stage_copy_mode: osgpu_set_stage_copy, else the environment)
 enum { STAGE_DMA = 0, STAGE_KOUT, STAGE_KERNEL };
-int stage_copy_mode()  // read per call (tests switch it between calls)
-{
-    const char *e = getenv("OSGPU_STAGE_COPY");
-    if (e && !strcmp(e, "kout")) return STAGE_KOUT;
-    if (e && !strcmp(e, "kernel")) return STAGE_KERNEL;
-    return STAGE_DMA;
-}
 
 // one staged leg: a kernel over the host side's device view (dview) when
 // the mode asks for one and the view exists, else the DMA engine
@@ -608,7 +607,7 @@ void run_staged(const Call &c, StageSet &S)
             }
             if (hi > lo) {
                 hipError_t e = osgpu::launch_team(c.type, c.op, P, dp.data(), sp.data(),
-                                                  (size_t) (hi - lo), S.st_c);
+                                                  (size_t) (hi - lo), S.st_c, S.ndev > 1);
                 if (e != hipSuccess) fatal(c.name, "team launch: %s", hipGetErrorString(e));
             }
         } else {  // large active sets: every PE folds its own chunk (pull form)
@@ -631,13 +630,6 @@ void run_staged(const Call &c, StageSet &S)
         memcpy(c.target, result, c.nbytes);
         free(result);
     }
-}
-
-size_t host_chunk_bytes()
-{
-    const char *e = getenv("OSGPU_HOST_CHUNK_BYTES");
-    size_t b = e ? strtoull(e, nullptr, 0) : 0;
-    return b ? b : (size_t) 64 << 20;
 }
 
 // Host symmetric-heap arguments: the data arrives and leaves through host
@@ -697,6 +689,38 @@ void run_host(const Call &c)
     }
 }
 
+// Small calls on HOST symmetric-heap memory (at most host_fold_max_bytes()
+// per PE, automatic host path): the reference's algorithm on this PE's
+// thread with the kernels' element ops compiled for the host (host_fold.hip)
+// -- the source copied into the target, barrier (src/reductions.c:82), every
+// other PE's whole source pulled with ONE shmem_getmem (the reference pulls
+// 64 elements per getmem, :90-103) and folded in this PE's order (:84-111),
+// barrier (:113), the temporary target copied back on overlap (:114-119).
+// No GPU round trip: below this size the fastest GPU form (one fused launch
+// reading and writing the host heap over PCIe) costs more than the whole
+// loop.
+void run_host_fold(const Call &c)
+{
+    t_last_path = OSGPU_RAN_HOST_FOLD;
+    const int P = c.PE_size;
+    std::vector<int> order(P);
+    fold_order(c.me, c.PE_start, c.step, P, order.data());
+    const bool overlap = ranges_overlap(c.target, c.source, c.nbytes);
+    thread_local std::vector<unsigned char> tmp, peer;
+    if (overlap) tmp.resize(c.nbytes);
+    void *acc = overlap ? (void *) tmp.data() : c.target;
+    memcpy(acc, c.source, c.nbytes);  // :79-81
+    barrier(c);                       // :82 -- every source is ready
+    peer.resize(c.nbytes);
+    for (int k = 1; k < P; k++) {     // order[0] is this PE
+        c.ops.getmem(peer.data(), c.source, c.nbytes, order[k]);
+        if (!osgpu::host_fold(c.type, c.op, acc, peer.data(), (size_t) c.nreduce))
+            fatal(c.name, "host fold: type %d op %d", c.type, c.op);
+    }
+    barrier(c);                       // :113 -- every peer is done reading my source
+    if (overlap) memcpy(c.target, acc, c.nbytes);  // :114-119
+}
+
 void to_all(const char *name, int type, int op, void *target, void *source, int nreduce,
             int PE_start, int logPE_stride, int PE_size, void *pWrk, long *pSync)
 {
@@ -721,13 +745,18 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     if (kt != ks)
         fatal(name, "target and source must both be device or both be host memory");
     if (kt == MEM_HOST) {
-        const char *hp = getenv("OSGPU_HOST_PATH");
-        const bool getmem_only = hp && !strcmp(hp, "getmem");
+        const int hp = host_path();
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
             fatal(name, "no GPU visible: the combine runs only on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
-        StageSet *S = getmem_only ? nullptr : stage_setup(c);
+        // a size every member shares: all of them take the same path
+        if (hp == OSGPU_HOST_AUTO && c.nbytes <= host_fold_max_bytes() &&
+            osgpu::host_fold_supported(type, op)) {
+            run_host_fold(c);
+            return;
+        }
+        StageSet *S = hp == OSGPU_HOST_GETMEM ? nullptr : stage_setup(c);
         // small calls on host heaps pinned with osgpu_host_register (on every
         // PE, like the heap itself): H2D, exchange and D2H in one launch
         void *hin = nullptr, *hout = nullptr;
@@ -756,6 +785,7 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     std::vector<const void *> srcs;
     std::vector<void *> dsts;
     int idx = -1;
+    bool remote = false;
     SyncSet *S = nullptr;
     // RCCL only where its result is the reference's: integer (type, op)s on
     // the automatic path when no device heap is registered; FP sum/prod only
@@ -763,14 +793,14 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
     // min/max never (they take the exact kernels even when RCCL is forced).
     if (mode == OSGPU_PATH_RCCL && rccl_usable(c, true)) {
         run_rccl(c);
-    } else if (mode != OSGPU_PATH_PULL && (idx = team_ptrs(c, srcs, dsts)) >= 0) {
+    } else if (mode != OSGPU_PATH_PULL && (idx = team_ptrs(c, srcs, dsts, &remote)) >= 0) {
         StageSet *G = nullptr;
         if (fused_eligible(c, true) && (S = sync_setup(c)))
             run_fused(c, *S, srcs, dsts, true);
         else if (team_exchange() == 1 && c.ops.getmem && (G = stage_setup(c)))
             run_team_push(c, srcs, dsts, idx, *G);
         else
-            run_team(c, srcs, dsts, idx);
+            run_team(c, srcs, dsts, idx, remote);
     } else if (member_sources(c, srcs)) {
         if (fused_eligible(c, false) && (S = sync_setup(c))) {
             run_fused(c, *S, srcs, dsts, false);

@@ -41,130 +41,90 @@ struct TeamPtrs {
 
 constexpr int kTeamBlock = 256;
 
-// above 4 members: U vectors per input per lane, G of them in flight per
-// round.  With the branch-free folds (elem_ops.hpp Fast), U = 4 in two
-// rounds of G = 2 (16 vectors of 16 B in flight per lane at 8 members)
-// beats one round of U = G = 2 at P = 8 for every type: float 0.715 ->
-// 0.786, complexf 0.723 -> 0.790 of 8 TB/s, int / long +2 %, the rest equal
-// (every build loaded in one process, interleaved on the same arrays,
-// profiles/r03_team_variants_interleaved.jsonl); U = G = 4 spills the
-// 8-input complexf fold (0.45).  The pull combine keeps OSGPU_U_K8
-#ifndef OSGPU_TEAM_U8
-#define OSGPU_TEAM_U8 4
-#endif
-#ifndef OSGPU_TEAM_G8
-#define OSGPU_TEAM_G8 2
-#endif
-// ... for the real (non-complex) types: one round of all U = 4 vectors
-// (their loads all in flight before the first fold; 3-6 waves per SIMD, no
-// scratch).  Against G = 2 in one process on the same allocations
-// (tools/team_inproc_ab.py, profiles/r05_team_p8_tile_ab.jsonl): 1.006x
-// over 7 (type, op) pairs at 5-8 members, floating-point folds 1.00-1.03x,
-// integer ones 0.996-1.004x.  The complex sum keeps G = 2 (G = 4 spills it)
+// ---------------------------------------------------------------- shapes
+// Tuning constants of the launch shapes.  Each was chosen by an in-process
+// A/B on the same allocations (tools/team_inproc_ab.py); the records are
+// cited here and in DESIGN_HISTORY.md.  The four left overridable with -D
+// (tools/build_ab.sh) are the ones a round-6 A/B still builds.
+//
+// Above 4 members: U vectors per input per lane, G of them in flight per
+// round.  U = 4 in two rounds of G = 2 (16 vectors of 16 B in flight per lane
+// at 8 members) beat one round of U = G = 2 at P = 8 for every type: float
+// 0.715 -> 0.786, complexf 0.723 -> 0.790 of 8 TB/s
+// (profiles/r03_team_variants_interleaved.jsonl); U = G = 4 spills the
+// 8-input complexf fold (0.45).
+constexpr int kTeamU8 = 4;
+constexpr int kTeamG8 = 2;  // complex sum; every type when members are remote
+// ... for the real (non-complex) types on one GPU: one round of all U = 4
+// vectors, 1.006x over 7 (type, op) pairs at 5-8 members
+// (profiles/r05_team_p8_tile_ab.jsonl).  Not measured across GPUs (xGMI):
+// calls with remote members keep G = kTeamG8 (TeamShape REMOTE).
 #ifndef OSGPU_TEAM_G8R
 #define OSGPU_TEAM_G8R 4
 #endif
 // the register-heavy folds above 4 members (complex products: 4-6 VALU
-// temporaries per element per output) take rounds of OSGPU_TEAM_GH vectors
-#ifndef OSGPU_TEAM_GH
-#define OSGPU_TEAM_GH 2
-#endif
-// 1: above 4 members, integer folds issue round r+1's loads before round
-// r's folds and stores (two round buffers), so a lane's loads stay in
-// flight while it stores; 0: round after round.  Integers only: for every
-// floating-point fold the two buffers cost 0.2-0.4 of the rate (the
-// compiler no longer keeps a round's loads in flight), against +0.5-1 % for
-// the integer ones (profiles/r04_team_type_op_sweep.jsonl)
-#ifndef OSGPU_TEAM_PIPE
-#define OSGPU_TEAM_PIPE 1
-#endif
-// floating-point folds on the two-buffer pipeline too: round 4 lost 0.2-0.4
-// of the rate to it because fold_store was not inlined and the round buffers
-// went to scratch; with the lambdas forced inline it compiles clean, and at
-// U = 6 / 8 (3 / 4 rounds of 2) ran 0.97-0.98x of the shipped tile (same
-// A/B file), so it stays off
-#ifndef OSGPU_TEAM_PIPE_FP
-#define OSGPU_TEAM_PIPE_FP 0
-#endif
-#ifndef OSGPU_TEAM_PIPE_FENCE
-#define OSGPU_TEAM_PIPE_FENCE 0
-#endif
-#ifndef OSGPU_TEAM_OCC_LDS
-#define OSGPU_TEAM_OCC_LDS 0
-#endif
-#ifndef OSGPU_TEAM_PEROUT
-#define OSGPU_TEAM_PEROUT 1
-#endif
-// from this many members on: the LDS-staged kernel (team_lds_kernel), one
-// wave per member.  2 members too: against the register form on the same
-// fresh allocations it ran 1.03x faster for double sum (20 allocations on
-// two leases, median 0.794 against 0.769 of 8 TB/s) and 1.00-1.07x for every
-// (type, op) probed -- float sum/prod, double max, int sum, long xor, short
-// min, complex sum/prod (profiles/r05_team_p2_ab.jsonl).
-// OSGPU_TEAM_LDS_U 16-B vectors per lane per tile.  U = 2
-// (2 KiB per member per workgroup): timed against U = 4 in one process on
-// the same fresh allocations (tools/team_inproc_ab.py, 10 allocations per
-// member count on each of two leases, profiles/r05_team_p34_ab.jsonl) it ran
-// 1.02-1.04x faster on average at 3 and 4 members and lifted the slowest
-// placement most (4 members: 0.749 against 0.683 of 8 TB/s), losing up to
-// 4 % only where the copy itself was fastest.  (Round 4 had chosen U = 4
-// from a sweep on one box: r04_team_sweep_3.jsonl.)  U = 8, 64 KiB of LDS
-// per workgroup at 8 members: 0.44-0.62, r04_team_sweep_2.jsonl
+// temporaries per element per output) take rounds of kTeamGH vectors
+constexpr int kTeamGH = 2;
+// Above 4 members integer folds issue round r+1's loads before round r's
+// folds and stores (two round buffers): +0.5-1 %; for floating-point folds
+// the two buffers cost 0.2-0.4 of the rate in round 4 and 2-3 % once inlined
+// (profiles/r04_team_type_op_sweep.jsonl, r05_team_p8_tile_ab.jsonl), so
+// only integers pipeline.  Ordered folds above 4 members fold, check and
+// store one output at a time (only one output vector live).
+// Vectors per input per lane for 2 and for 3-4 members in the register form
+// (all loaded before the first fold): U = 2 at 2 members ran 0.71-0.75
+// against 0.77 with U = 4.
+constexpr int kTeamU2 = 4;
+constexpr int kTeamU4 = 4;
+// The LDS-staged kernel (team_lds_kernel, one wave per member) serves
+// OSGPU_TEAM_LDS_MIN_P .. OSGPU_TEAM_LDS_MAX_P members.  2 members: 1.03x
+// over the register form for double sum, 1.00-1.07x for every (type, op)
+// probed (profiles/r05_team_p2_ab.jsonl); 3-4 members ahead or equal on
+// every box; 5-8 members: the register form's best (0.81 of 8 TB/s at 8) is
+// above the LDS form's (0.75) (r04_team_place_3/4.jsonl).  Calls with
+// remote members keep the round-4 range, 3-4 (TeamShape REMOTE): the 2-member
+// A/B ran on one GPU only.
 #ifndef OSGPU_TEAM_LDS_MIN_P
 #define OSGPU_TEAM_LDS_MIN_P 2
 #endif
-// ... up to this many members; above, the register form.  On boxes whose
-// P-range copy itself is fast (0.81-0.84 of 8 TB/s) the register form led
-// at 5-8 members by 5-7 % (0.956 against 0.884 of the copy at 8, five
-// allocations, order rotated, r04_team_place_4.jsonl), on slow ones (0.75-
-// 0.77) the LDS form by 3-5 % (r04_team_place_3.jsonl): in absolute terms
-// the register form's best (0.81 of 8 TB/s at 8 members) is above the LDS
-// form's (0.75), so it keeps 5-8; at 3-4 members the LDS form is ahead or
-// equal on both kinds of box
 #ifndef OSGPU_TEAM_LDS_MAX_P
 #define OSGPU_TEAM_LDS_MAX_P 4
 #endif
+// 16-B vectors per lane per LDS tile: U = 2 (2 KiB per member per workgroup)
+// 1.02-1.04x over U = 4 at 3-4 members (profiles/r05_team_p34_ab.jsonl).
+// Round 6 (profiles/r06_team_p4_ab.jsonl, 5 allocations each, 4 members):
+// U = 2 staged by LDS-DMA (global_load_lds_dwordx4) 0.998x of this form, U = 4
+// by LDS-DMA 0.967x, LDS-DMA without the nt bit 0.982x, the register form
+// 0.986x; this form ran 0.98 of the same-mix copy there.
 #ifndef OSGPU_TEAM_LDS_U
 #define OSGPU_TEAM_LDS_U 2
 #endif
-#ifndef OSGPU_TEAM_LDS_U8
-#define OSGPU_TEAM_LDS_U8 4
-#endif
-#ifndef OSGPU_TEAM_LDS_ROT
-#define OSGPU_TEAM_LDS_ROT 0
-#endif
 
-
-// vectors per input per lane for 2 and for 3-4 members (all loaded before
-// the first fold).  U = 2 at 2 members: 0.71-0.75 against 0.77 with U = 4
-// (same interleaved A/B)
-#ifndef OSGPU_TEAM_U2
-#define OSGPU_TEAM_U2 OSGPU_U_K2
-#endif
-#ifndef OSGPU_TEAM_U4
-#define OSGPU_TEAM_U4 OSGPU_U_K4
-#endif
-
-// Launch shape per (T, OP, P): U vectors per input per lane in rounds of G
-template <typename T, int OP, int P>
+// Launch shape per (T, OP, P): U vectors per input per lane in rounds of G.
+// REMOTE: some member's arrays live in another GPU's HBM (xGMI): the shapes
+// last measured across GPUs (round 4) -- the register form at 2 members and
+// rounds of kTeamG8 above 4.
+template <typename T, int OP, int P, bool REMOTE = false>
 struct TeamShape {
-    static constexpr bool kHeavy = (std::is_same<T, cfloat>::value || std::is_same<T, cdouble>::value) &&
-                                   OP == OP_PROD;
-    static constexpr int U = P <= 2 ? OSGPU_TEAM_U2 : (P <= 4 ? OSGPU_TEAM_U4 : OSGPU_TEAM_U8);
     static constexpr bool kComplex = std::is_same<T, cfloat>::value || std::is_same<T, cdouble>::value;
-    static constexpr int G = P <= 4 ? U : (kHeavy ? OSGPU_TEAM_GH : (kComplex ? OSGPU_TEAM_G8 : OSGPU_TEAM_G8R));
-    static constexpr bool kPipe = P > 4 && OSGPU_TEAM_PIPE && U / G > 1 &&
-                                  (std::is_integral<T>::value || OSGPU_TEAM_PIPE_FP);
-    // ordered folds above 4 members: fold, check and store one output at a
-    // time instead of all P outputs, then all P stores
-    static constexpr bool kPerOutput = P > 4 && OSGPU_TEAM_PEROUT;
-    static constexpr bool kLds = P >= OSGPU_TEAM_LDS_MIN_P && P <= OSGPU_TEAM_LDS_MAX_P &&
-                                 !(std::is_same<T, cdouble>::value && OP == OP_PROD && P >= 8);
-    static constexpr int kLdsU = P >= 8 ? OSGPU_TEAM_LDS_U8 : OSGPU_TEAM_LDS_U;
+    static constexpr bool kHeavy = kComplex && OP == OP_PROD;
+    static constexpr int U = P <= 2 ? kTeamU2 : (P <= 4 ? kTeamU4 : kTeamU8);
+    static constexpr int G = P <= 4 ? U
+                             : (kHeavy ? kTeamGH : ((kComplex || REMOTE) ? kTeamG8 : OSGPU_TEAM_G8R));
+    static constexpr bool kPipe = P > 4 && U / G > 1 && std::is_integral<T>::value;
+    static constexpr bool kPerOutput = P > 4;
+    static constexpr bool kLds = REMOTE ? (P >= 3 && P <= 4)
+                                        : (P >= OSGPU_TEAM_LDS_MIN_P && P <= OSGPU_TEAM_LDS_MAX_P);
+    static constexpr int kLdsU = OSGPU_TEAM_LDS_U;
     // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
     // round reads and writes past the tile (and past nvec)
     static_assert(G >= 1 && G <= U && U % G == 0, "the round size must divide U");
 };
+
+// the remote shape differs from the local one (else the local kernel serves)
+template <typename T, int OP, int P>
+constexpr bool kRemoteDiffers = TeamShape<T, OP, P, true>::kLds != TeamShape<T, OP, P, false>::kLds ||
+                                TeamShape<T, OP, P, true>::G != TeamShape<T, OP, P, false>::G;
 
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction
 // (a #pragma unroll on the round loop is dropped for the largest bodies)
@@ -180,24 +140,10 @@ struct Rounds {
     }
 };
 
-// XCD-aware workgroup -> tile map (OSGPU_TEAM_XCD, off): the dispatcher
-// deals workgroups round-robin over the 8 XCDs (b % 8), so with the identity
-// map XCD x streams tiles x, x + 8, x + 16, ...; remapped, XCD x streams one
-// contiguous run of tiles.  A bijection on [0, n) for any n.  Measured
-// slower at every member count over ten array layouts (of the same-mix
-// copy: 2 members 0.954 vs 0.978 median, 4 members 0.934 vs 0.962, 8
-// members 0.853 vs 0.886; tools/team_layout_sweep.py,
-// profiles/r05_team_layouts.jsonl), so the identity map ships.
-#ifndef OSGPU_TEAM_XCD
-#define OSGPU_TEAM_XCD 0
-#endif
-constexpr unsigned kXcds = 8;
-__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned n)
-{
-    if (!OSGPU_TEAM_XCD || n < kXcds) return b;
-    const unsigned x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
-    return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
-}
+// (An XCD-aware workgroup -> tile map -- XCD x streaming one contiguous run of
+// tiles instead of tiles x, x + 8, ... -- ran slower at every member count
+// over ten layouts, 0.853-0.954 against 0.886-0.978 of the same-mix copy,
+// profiles/r05_team_layouts.jsonl: the identity map ships.)
 
 // E: Elem<T, OP> (exact) or Fast<T, OP> (branch-free, elem_ops.hpp)
 template <typename T, int OP, int P, bool ORDERED, typename E = Elem<T, OP>>
@@ -221,24 +167,14 @@ __device__ __forceinline__ void team_fold(const T (&x)[P], T (&r)[P])
     }
 }
 
-template <typename T, int OP, int P, bool ORDERED>
+template <typename T, int OP, int P, bool ORDERED, bool REMOTE>
 __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, size_t nvec,
                                                               size_t head, size_t tail_start,
                                                               int nedge, unsigned tm, unsigned tk)
 {
     constexpr int W = 16 / sizeof(T);
-    using S = TeamShape<T, OP, P>;
+    using S = TeamShape<T, OP, P, REMOTE>;
     constexpr int U = S::U;
-#if OSGPU_TEAM_OCC_LDS
-    // occupancy cap (experiment): a workgroup holds this much LDS, so at
-    // most 160 KiB / OSGPU_TEAM_OCC_LDS workgroups share a CU.  3 or 4
-    // workgroups per CU at 6 / 8 members: 0.99-1.00x (same A/B file)
-    if constexpr (P > 4) {
-        __shared__ unsigned occ_pad[OSGPU_TEAM_OCC_LDS / 4];
-        if (nvec == 0) reinterpret_cast<volatile unsigned *>(occ_pad)[threadIdx.x] = 0;
-        __syncthreads();
-    }
-#endif
     if (blockIdx.x == 0 && (int) threadIdx.x < nedge) {
         const size_t e = threadIdx.x < head ? threadIdx.x : tail_start + (threadIdx.x - head);
         T x[P], r[P];
@@ -249,8 +185,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
     // tile blockIdx.x * tm + tk (launch_team_tiles; tm = 1, tk = 0: tile blockIdx.x)
-    const size_t t0 = ((size_t) xcd_tile(blockIdx.x, gridDim.x) * tm + tk) * (kTeamBlock * U) +
-                      threadIdx.x;
+    const size_t t0 = ((size_t) blockIdx.x * tm + tk) * (kTeamBlock * U) + threadIdx.x;
     // fold one vector of every input into one vector of every output: the
     // branch-free fold first, the exact one only for a vector whose results
     // hold a NaN part (rare; elem_ops.hpp Fast) -- no branch per element, so
@@ -340,12 +275,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_vec_kernel(TeamPtrs<T, P> a, 
                 constexpr int r = decltype(rc)::value;
                 auto &cur = (r % 2 == 0) ? b0 : b1;
                 auto &nxt = (r % 2 == 0) ? b1 : b0;
-                if constexpr (r + 1 < R) {
-                    load_round(nxt, r + 1);
-                    // keep the scheduler from sinking these loads below the
-                    // stores (it does, to save registers, when it may)
-                    if constexpr (OSGPU_TEAM_PIPE_FENCE) asm volatile("" ::: "memory");
-                }
+                if constexpr (r + 1 < R) load_round(nxt, r + 1);
 #pragma unroll
                 for (int u = 0; u < G; u++) fold_store(cur[u], t0 + (size_t) (r * G + u) * kTeamBlock);
             });
@@ -412,15 +342,8 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
 #pragma unroll
         for (int p = 0; p < P; p++) a.dst[p][e] = r[p];
     }
-    const int wave = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
-    // the member this wave stages and writes: wave w, or with
-    // OSGPU_TEAM_LDS_ROT member (w + blockIdx.x) % P (the waves of
-    // neighbouring workgroups start on different arrays)
-#if OSGPU_TEAM_LDS_ROT
-    const int w = __builtin_amdgcn_readfirstlane((int) ((wave + blockIdx.x) % P));
-#else
-    const int w = wave;
-#endif
+    // the member this wave stages and writes
+    const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6));
     const int lane = (int) (threadIdx.x & 63);
     const u32x4 *src = reinterpret_cast<const u32x4 *>(pick(a.src, w) + head);
     u32x4 *dst = reinterpret_cast<u32x4 *>(pick(a.dst, w) + head);
@@ -473,7 +396,7 @@ __global__ __launch_bounds__(64 * P) void team_lds_kernel(TeamPtrs<T, P> a, size
             }
         });
     };
-    const size_t t = (size_t) xcd_tile(blockIdx.x, gridDim.x) * tm + tk;
+    const size_t t = (size_t) blockIdx.x * tm + tk;
     load(t);
 #pragma unroll
     for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
@@ -501,6 +424,7 @@ __global__ __launch_bounds__(kTeamBlock) void team_scalar_kernel(TeamPtrs<T, P> 
 // tiles of m members, this one k-th (launch_team_tiles)
 struct Tiles {
     unsigned m, k;
+    bool remote;  // some member's arrays are in another GPU's HBM
     // of `total` tiles, the ones this member folds (at least one block)
     size_t blocks(size_t total) const
     {
@@ -509,10 +433,11 @@ struct Tiles {
     }
 };
 
-template <typename T, int OP, int P>
+template <typename T, int OP, int P, bool REMOTE>
 static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size_t n,
                                 Tiles tl, hipStream_t s)
 {
+    using S = TeamShape<T, OP, P, REMOTE>;
     // integer ops are order-independent (wrapping ring / lattice ops); every
     // floating-point op, min/max included (NaN, signed zero), is not
     constexpr bool ORDERED = !std::is_integral<T>::value;
@@ -538,19 +463,29 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
     const size_t tail_start = head + nvec * W;
     // the unaligned head and the tail: member 0's first workgroup
     const int nedge = tl.k == 0 ? (int) (head + (n - tail_start)) : 0;
-    if constexpr (TeamShape<T, OP, P>::kLds) {
-        constexpr int UL = TeamShape<T, OP, P>::kLdsU;
+    if constexpr (S::kLds) {
+        constexpr int UL = S::kLdsU;
         const size_t blocks = tl.blocks((nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL));
         hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
                            dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
     } else {  // (not instantiated where the LDS form is used)
-        constexpr int U = TeamShape<T, OP, P>::U;
+        constexpr int U = S::U;
         const size_t blocks =
             tl.blocks((nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U));
-        hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED>), dim3((unsigned) blocks),
+        hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED, REMOTE>), dim3((unsigned) blocks),
                            dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
     }
     return hipGetLastError();
+}
+
+// the remote shape only where it differs from the local one
+template <typename T, int OP, int P>
+static hipError_t team_launch_pr(void *const *d, const void *const *sr, size_t n, Tiles tl,
+                                 hipStream_t s)
+{
+    if constexpr (kRemoteDiffers<T, OP, P>)
+        if (tl.remote) return team_launch_p<T, OP, P, true>(d, sr, n, tl, s);
+    return team_launch_p<T, OP, P, false>(d, sr, n, tl, s);
 }
 
 template <typename T, int OP>
@@ -558,13 +493,13 @@ static hipError_t team_launch_op(int P, void *const *d, const void *const *sr, s
                                  Tiles tl, hipStream_t s)
 {
     switch (P) {
-    case 2: return team_launch_p<T, OP, 2>(d, sr, n, tl, s);
-    case 3: return team_launch_p<T, OP, 3>(d, sr, n, tl, s);
-    case 4: return team_launch_p<T, OP, 4>(d, sr, n, tl, s);
-    case 5: return team_launch_p<T, OP, 5>(d, sr, n, tl, s);
-    case 6: return team_launch_p<T, OP, 6>(d, sr, n, tl, s);
-    case 7: return team_launch_p<T, OP, 7>(d, sr, n, tl, s);
-    case 8: return team_launch_p<T, OP, 8>(d, sr, n, tl, s);
+    case 2: return team_launch_pr<T, OP, 2>(d, sr, n, tl, s);
+    case 3: return team_launch_pr<T, OP, 3>(d, sr, n, tl, s);
+    case 4: return team_launch_pr<T, OP, 4>(d, sr, n, tl, s);
+    case 5: return team_launch_pr<T, OP, 5>(d, sr, n, tl, s);
+    case 6: return team_launch_pr<T, OP, 6>(d, sr, n, tl, s);
+    case 7: return team_launch_pr<T, OP, 7>(d, sr, n, tl, s);
+    case 8: return team_launch_pr<T, OP, 8>(d, sr, n, tl, s);
     }
     return hipErrorInvalidValue;
 }
@@ -604,11 +539,11 @@ static hipError_t team_cplx(int op, int P, void *const *d, const void *const *sr
 }
 
 hipError_t launch_team_tiles(int type, int op, int P, void *const *dsts, const void *const *srcs,
-                             size_t n, int m, int k, hipStream_t s)
+                             size_t n, int m, int k, hipStream_t s, bool remote)
 {
     if (P < 2 || P > kMaxTeam || m < 1 || k < 0 || k >= m) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
-    const Tiles tl{(unsigned) m, (unsigned) k};
+    const Tiles tl{(unsigned) m, (unsigned) k, remote};
     switch (type) {
     case T_SHORT: return team_int<int16_t>(op, P, dsts, srcs, n, tl, s);
     case T_INT: return team_int<int32_t>(op, P, dsts, srcs, n, tl, s);
@@ -625,9 +560,9 @@ hipError_t launch_team_tiles(int type, int op, int P, void *const *dsts, const v
 }
 
 hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
-                       size_t n, hipStream_t s)
+                       size_t n, hipStream_t s, bool remote)
 {
-    return launch_team_tiles(type, op, P, dsts, srcs, n, 1, 0, s);
+    return launch_team_tiles(type, op, P, dsts, srcs, n, 1, 0, s, remote);
 }
 
 }  // namespace osgpu

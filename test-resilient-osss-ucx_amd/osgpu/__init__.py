@@ -32,7 +32,8 @@ CTYPE = {
 PATH_AUTO, PATH_P2P, PATH_RCCL, PATH_PULL = 0, 1, 2, 3
 # enum osgpu_ran: what osgpu_last_path() reports
 RAN = ["none", "team", "pull", "rccl", "staged", "getmem", "fused_team", "fused_pull",
-       "barrier_only", "fused_staged", "copy", "fused_copy", "fused_failed", "team_push"]
+       "barrier_only", "fused_staged", "copy", "fused_copy", "fused_failed", "team_push",
+       "host_fold"]
 
 
 def has_op(t: str, op: str) -> bool:
@@ -146,6 +147,11 @@ def load() -> ctypes.CDLL:
     L.osgpu_set_fused_max_bytes.argtypes = [ctypes.c_longlong]
     L.osgpu_set_device_barrier.argtypes = [ctypes.c_double, ctypes.c_int]
     L.osgpu_set_team_exchange.argtypes = [ctypes.c_int]
+    L.osgpu_set_host_path.argtypes = [ctypes.c_int]
+    L.osgpu_set_host_fold_max_bytes.argtypes = [ctypes.c_longlong]
+    L.osgpu_set_stage_copy.argtypes = [ctypes.c_int]
+    L.osgpu_set_host_chunk_bytes.argtypes = [ctypes.c_longlong]
+    L.osgpu_set_stage_bytes.argtypes = [ctypes.c_longlong]
     L.osgpu_checksum.argtypes = [i, i, vp, sz, vp, ctypes.POINTER(ctypes.c_ulonglong)]
     L.osgpu_compare.argtypes = [vp, vp, sz, vp, ctypes.POINTER(ctypes.c_ulonglong),
                                 ctypes.POINTER(ctypes.c_ulonglong)]
@@ -158,6 +164,28 @@ def load() -> ctypes.CDLL:
 
 
 CK_SUM, CK_XOR, CK_HASH = 0, 1, 2
+
+# osgpu_set_host_path modes (include/osgpu_reduce.h enum osgpu_host_path)
+HOST_AUTO, HOST_STAGED, HOST_GETMEM = 0, 1, 2
+HOST_PATHS = {"auto": HOST_AUTO, "staged": HOST_STAGED, "getmem": HOST_GETMEM}
+STAGE_COPY = {"dma": 0, "kout": 1, "kernel": 2}
+
+
+class host_path:
+    """with osgpu.host_path("staged" | "getmem" | "auto" | None): the host
+    symmetric-heap path for the block (None: the environment's default),
+    restored to the environment's default afterwards."""
+
+    def __init__(self, mode):
+        self.mode = -1 if mode is None else HOST_PATHS[mode]
+
+    def __enter__(self):
+        assert load().osgpu_set_host_path(self.mode) == 0
+        return self
+
+    def __exit__(self, *exc):
+        load().osgpu_set_host_path(-1)
+        return False
 
 
 def checksum(t: str, mode: int, ptr: int, n: int, stream: int | None = None) -> int:

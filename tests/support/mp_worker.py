@@ -127,11 +127,11 @@ def finalize_cycle_mode(L, PES, rank, world, cycles=4):
             else:
                 ctypes.memmove(hbase, raw.ctypes.data, raw.size)
                 src, tgt = hbase, hbase + (4 << 20)
-                os.environ["OSGPU_HOST_PATH"] = "staged"
+                L.osgpu_set_host_path(osgpu.HOST_STAGED)
             PES.pes_barrier(0, 0, world, None)
             L.shmem_double_sum_to_all(tgt, src, n, 0, 0, world, wrk, psync)
             ran = osgpu.last_path()
-            os.environ.pop("OSGPU_HOST_PATH", None)
+            L.osgpu_set_host_path(-1)
             if dev:
                 out_t = torch.empty(n * 8, dtype=torch.uint8, device="cuda:0")
                 osgpu.copy([out_t.data_ptr()], [tgt], [n * 8])
@@ -250,9 +250,11 @@ def preflight_mode(L, PES, rank, world):
     dist.barrier()
     # a planted wrong mapping (heap.cpp test hook): PE 0 reaches PE 1's heap
     # chunks and staging through PE 2's ranges
+    os.environ["OSGPU_TEST_HOOKS"] = "1"   # tests/support/osgpu_test_hooks.h
     assert L.osgpu_test_preflight_fault(0, 1) == 0
     rc_fault, rep_fault = osgpu.preflight(base, 0, 0, world, psync)
     assert L.osgpu_test_preflight_fault(-1, -1) == 0
+    os.environ.pop("OSGPU_TEST_HOOKS", None)
     dist.barrier()
     assert L.osgpu_heap_destroy(ctypes.c_void_p(base)) == 0
     return {"preflight_rc": rc, "preflight": rep, "preflight_none_rc": rc_none,
@@ -836,9 +838,9 @@ def device_heap_modes(L, PES, mode, rank, world):
             host = ci.endswith("/host")
             # host heaps: forced staging (small calls stay on getmem otherwise)
             if host:
-                os.environ["OSGPU_HOST_PATH"] = "staged"
+                L.osgpu_set_host_path(osgpu.HOST_STAGED)
             else:
-                os.environ.pop("OSGPU_HOST_PATH", None)
+                L.osgpu_set_host_path(-1)
             b0 = hbase if host else dev0
             npes, start, log, size = c["set"]
             if npes > world:
@@ -868,7 +870,7 @@ def device_heap_modes(L, PES, mode, rank, world):
                 digests[ci] = hashlib.sha256(got.tobytes()).hexdigest()
             sync()
         L.osgpu_set_fused_max_bytes(-1)
-        os.environ.pop("OSGPU_HOST_PATH", None)
+        L.osgpu_set_host_path(-1)
         assert L.osgpu_host_unregister(ctypes.c_void_p(hbase)) == 0
         res["digests"], res["paths"] = digests, paths
     if mode == "golden":
@@ -1006,8 +1008,12 @@ def device_heap_modes(L, PES, mode, rank, world):
             src_h = np.ctypeslib.as_array((ctypes.c_int32 * n).from_address(hbase))
             src_h[:] = np.arange(n, dtype=np.int32) + rank
             assert L.osgpu_host_register(ctypes.c_void_p(hbase), 1 << 23) == 0
-            for name, lim in (("host_staged", 0), ("host_fused_staged", 1 << 30)):
+            # host_fold: the library's default for host-heap calls of at most
+            # its limit (64 KiB per PE), forced on at every size here
+            for name, lim, fold in (("host_staged", 0, 0), ("host_fused_staged", 1 << 30, 0),
+                                    ("host_fold", 0, 1 << 30)):
                 L.osgpu_set_fused_max_bytes(lim)
+                L.osgpu_set_host_fold_max_bytes(fold)
                 ts = []
                 for r in range(reps + 5):
                     sync()
@@ -1018,9 +1024,16 @@ def device_heap_modes(L, PES, mode, rank, world):
                 got = np.ctypeslib.as_array((ctypes.c_int32 * n).from_address(hbase + toff))
                 ok = bool(np.array_equal(got, world * np.arange(n, dtype=np.int32)
                                          + world * (world - 1) // 2))
+                ran = osgpu.last_path()
+                fnp = ctypes.cast(L.shmem_int_sum_to_all, ctypes.c_void_p)
+                tc = PES.pes_time_to_all(fnp, ctypes.c_void_p(hbase + toff), ctypes.c_void_p(hbase),
+                                         n, 0, 0, world, ctypes.c_void_p(ctypes.addressof(wrk)),
+                                         ctypes.c_void_p(psync), reps)
                 lat[f"{n}/{name}"] = {"us_median": float(np.median(ts[5:]) * 1e6),
+                                      "us_median_timed_in_c": tc * 1e6,
                                       "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
-                                      "path": osgpu.last_path(), "correct": ok}
+                                      "path": ran, "correct": ok}
+            L.osgpu_set_host_fold_max_bytes(0)
             # the collectives on the same pinned host heap: the runtime's
             # getmem (the default for small calls) vs the forced one-launch
             # staged copy
@@ -1032,7 +1045,7 @@ def device_heap_modes(L, PES, mode, rank, world):
                     for name, lim in (("host_getmem", 0), ("host_fused_staged", 1 << 30)):
                         L.osgpu_set_fused_max_bytes(lim)
                         if lim:  # the one-launch staged form needs staging forced
-                            os.environ["OSGPU_HOST_PATH"] = "staged"
+                            L.osgpu_set_host_path(osgpu.HOST_STAGED)
                         ts = []
                         for r in range(reps + 5):
                             sync()
@@ -1043,7 +1056,7 @@ def device_heap_modes(L, PES, mode, rank, world):
                                 f(hbase + coff, hbase, ne, 0, 0, world, psync)
                             sync()
                             ts.append(time.perf_counter() - t0)
-                        os.environ.pop("OSGPU_HOST_PATH", None)
+                        L.osgpu_set_host_path(-1)
                         lat[f"{n}/{kind}32_{name}"] = {
                             "us_median": float(np.median(ts[5:]) * 1e6),
                             "us_p10": float(np.percentile(ts[5:], 10) * 1e6),
@@ -1099,7 +1112,7 @@ def mixpush_mode(L, PES, rank, world, iters=24):
     heap[: nd * 8].copy_(torch.from_numpy(np.ascontiguousarray(dsrc[rank]).view(np.uint8).copy()))
     dtoff = 4 << 20
     torch.cuda.synchronize()
-    os.environ["OSGPU_HOST_PATH"] = "staged"
+    L.osgpu_set_host_path(osgpu.HOST_STAGED)
     L.osgpu_set_fused_max_bytes(0)          # host barriers: the staged pipeline
     rng = random.Random(rank * 7919 + 1)
     bad = {"host": 0, "device": 0}
@@ -1126,7 +1139,7 @@ def mixpush_mode(L, PES, rank, world, iters=24):
         torch.cuda.synchronize()
     L.osgpu_set_team_exchange(-1)
     L.osgpu_set_fused_max_bytes(-1)
-    os.environ.pop("OSGPU_HOST_PATH", None)
+    L.osgpu_set_host_path(-1)
     dist.barrier()
     L.osgpu_finalize()
     for p in mapped:
@@ -1139,6 +1152,9 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     L = osgpu.load()
+    # small host-heap calls on the GPU paths (the host fold off) unless the
+    # mode measures or checks the host fold itself
+    L.osgpu_set_host_fold_max_bytes(-1 if os.environ.get("MP_HOST_FOLD") == "1" else 0)
     counter = [0]
     PES = None
     if os.environ.get("OSGPU_TEST_PES", "gloo") == "shm" or mode in (
@@ -1172,8 +1188,12 @@ def main():
                 if pinned:
                     assert L.osgpu_host_register(ctypes.c_void_p(base), 1 << 24) == 0
                 for hp, inplace, fused in (("staged", False, -1), ("staged", True, -1),
-                                           ("staged", False, 0), ("getmem", False, -1)):
-                    os.environ["OSGPU_HOST_PATH"] = hp
+                                           ("staged", False, 0), ("getmem", False, -1),
+                                           ("fold", False, -1), ("fold", True, -1)):
+                    # fold: the automatic path with the host fold on (the
+                    # library's default for small host-heap calls)
+                    L.osgpu_set_host_path(osgpu.HOST_PATHS.get(hp, osgpu.HOST_AUTO))
+                    L.osgpu_set_host_fold_max_bytes(-1 if hp == "fold" else 0)
                     L.osgpu_set_fused_max_bytes(fused)
                     ctypes.memmove(base, raw.ctypes.data, raw.size)
                     tgt = base + (0 if inplace else toff)
@@ -1190,12 +1210,13 @@ def main():
                 if pinned:
                     assert L.osgpu_host_unregister(ctypes.c_void_p(base)) == 0
             L.osgpu_set_fused_max_bytes(-1)
+            L.osgpu_set_host_fold_max_bytes(0)
         for hp in ("staged", "getmem"):
-            os.environ["OSGPU_HOST_PATH"] = hp
+            L.osgpu_set_host_path(osgpu.HOST_PATHS[hp])
             run_colls(L, rank, world, base, base + (1 << 22), psync, out, hp,
                       lambda off, raw: ctypes.memmove(off, raw.ctypes.data, raw.size),
                       lambda off, nb: np.frombuffer(ctypes.string_at(off, nb), np.uint8))
-        os.environ.pop("OSGPU_HOST_PATH", None)
+        L.osgpu_set_host_path(-1)
         res["out"] = out
     if mode == "mixpush":
         res.update(mixpush_mode(L, PES, rank, world))

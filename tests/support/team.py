@@ -50,7 +50,11 @@ def _align(x, a=256):
 class Team:
     """npes PEs, each with `heap_bytes` of symmetric heap (device or host)."""
 
-    def __init__(self, npes: int, heap_bytes: int, device: bool = True):
+    def __init__(self, npes: int, heap_bytes: int, device: bool = True, host_fold: bool = False):
+        """host_fold=False: small host-heap calls take the GPU paths (the
+        host fold's limit set to 0) -- the GPU tests exercise those; True:
+        the library's default, small host-heap calls folded on the host
+        (shmem_reduce.cpp run_host_fold)."""
         import osgpu
         self.lib = osgpu.load()
         self.osgpu = osgpu
@@ -60,6 +64,7 @@ class Team:
         self.H = _align(heap_bytes) + 4096
         self.psync_off = self.H - 4096
         self.device = device
+        self.host_fold = host_fold
         if device:
             import torch
             self.torch = torch
@@ -84,6 +89,7 @@ class Team:
         device heaps, host heaps (the pSync heap of a device team)."""
         assert self.pet.pet_init(self.npes) == 0
         assert self.lib.osgpu_set_pe_ops(self.pet.pet_ops()) == 0
+        assert self.lib.osgpu_set_host_fold_max_bytes(-1 if self.host_fold else 0) == 0
         for pe in range(64):
             self.lib.osgpu_heap_unregister(pe)
         for pe in range(self.npes):

@@ -270,3 +270,14 @@ def test_missing_runtime_is_reported():
                        timeout=300)
     assert r.returncode != 0
     assert "no OpenSHMEM runtime" in r.stderr
+
+
+def test_test_hook_refused_in_production(lib, monkeypatch):
+    """the preflight fault hook is not in the public header and
+    is refused unless the process enables test hooks (OSGPU_TEST_HOOKS=1)."""
+    monkeypatch.delenv("OSGPU_TEST_HOOKS", raising=False)
+    hdr = open(os.path.join(ROOT, "include", "osgpu_reduce.h")).read()
+    assert "osgpu_test_preflight_fault" not in hdr
+    lib.osgpu_test_preflight_fault.argtypes = [ctypes.c_int, ctypes.c_int]
+    assert lib.osgpu_test_preflight_fault(0, 1) != 0
+    assert b"test hooks are off" in lib.osgpu_last_error()

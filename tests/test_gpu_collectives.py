@@ -9,7 +9,6 @@ device staging -> D2H), also with tiny staging slots to force many chunks,
 and the GETMEM path.  Every byte of every member's target region is compared,
 including the margins the collective must not write; pSync must come back at
 SHMEM_SYNC_VALUE (checked by Team)."""
-import contextlib
 import os
 
 import numpy as np
@@ -26,19 +25,10 @@ MARGIN = 256
 MODES = ["device", "host", "staged"]  # host = auto (GETMEM when PEs share a GPU)
 
 
-@contextlib.contextmanager
 def host_path(mode):
-    """OSGPU_HOST_PATH for the duration of a case (read on every call)."""
-    old = os.environ.get("OSGPU_HOST_PATH")
-    if mode in ("staged", "getmem"):
-        os.environ["OSGPU_HOST_PATH"] = mode
-    try:
-        yield
-    finally:
-        if old is None:
-            os.environ.pop("OSGPU_HOST_PATH", None)
-        else:
-            os.environ["OSGPU_HOST_PATH"] = old
+    """osgpu_set_host_path for the duration of a case (staged / getmem;
+    anything else: the automatic path)."""
+    return osgpu.host_path(mode if mode in ("staged", "getmem") else None)
 
 
 def _layout(P, max_src_bytes):
@@ -159,14 +149,14 @@ def test_host_staged_many_chunks(kind):
     """16 KiB of staging per PE: thousands of chunks, ragged last chunk."""
     L = osgpu.load()
     L.osgpu_finalize()
-    os.environ["OSGPU_STAGE_BYTES"] = "4096"
+    L.osgpu_set_stage_bytes(4096)
     try:
         with host_path("staged"):
             _run_case(False, kind, 32, (4, 0, 0, 4), 30011, root=3, seed=9)
             _run_case(False, kind, 64, (8, 1, 1, 3), 9001, root=2, seed=10)
     finally:
         L.osgpu_finalize()
-        del os.environ["OSGPU_STAGE_BYTES"]
+        L.osgpu_set_stage_bytes(-1)
 
 
 @pytest.mark.parametrize("kind", ["broadcast", "collect", "fcollect", "alltoall"])

@@ -37,12 +37,13 @@ def torch_cuda():
 _TEAMS = {}
 
 
-def team(device=True):
+def team(device=True, host_fold=False):
     from support import team as T
     key = device
     if key not in _TEAMS:
         _TEAMS[key] = T.Team(8, 20 << 20, device=device)
     tm = _TEAMS[key]
+    tm.host_fold = host_fold   # the library default (True) or the GPU paths
     tm.activate()
     return tm
 
@@ -116,7 +117,7 @@ def test_team_push_matches_golden(torch_cuda):
     tm = team(device=True)
     L = tm.lib
     L.osgpu_finalize()
-    os.environ["OSGPU_STAGE_BYTES"] = "65536"
+    L.osgpu_set_stage_bytes(65536)
     L.osgpu_set_team_exchange(1)
     try:
         for c in CASES:
@@ -128,7 +129,7 @@ def test_team_push_matches_golden(torch_cuda):
     finally:
         L.osgpu_set_team_exchange(-1)
         L.osgpu_finalize()
-        del os.environ["OSGPU_STAGE_BYTES"]
+        L.osgpu_set_stage_bytes(-1)
 
 
 def test_pull_path_matches_golden(torch_cuda):
@@ -165,22 +166,60 @@ def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
     GPU through the staging buffers -> D2H, 4 KiB chunks so the two-slot
     pipeline turns over many times; getmem: every peer's source pulled
     through the runtime's shmem_getmem (the reference's transport)."""
-    monkeypatch.setenv("OSGPU_HOST_CHUNK_BYTES", "4096")  # many chunks
-    monkeypatch.setenv("OSGPU_STAGE_BYTES", "4096")
-    monkeypatch.setenv("OSGPU_HOST_PATH", host_path)
-    osgpu.load().osgpu_finalize()  # staging is sized at set-up
-    tm = team(device=False)
-    n = 0
+    L = osgpu.load()
+    L.osgpu_set_host_chunk_bytes(4096)  # many chunks
+    L.osgpu_set_stage_bytes(4096)
+    L.osgpu_finalize()  # staging is sized at set-up
+    try:
+        with osgpu.host_path(host_path):
+            tm = team(device=False)
+            n = 0
+            for c in CASES:
+                if c["type"] == t and c["op"] == op and c["nreduce"] <= 4097 and \
+                        c["npes"] in (1, 2, 3, 8):
+                    check(c, run_case(tm, c))
+                    if c["nreduce"] > 0 and c["npes"] > 1:
+                        assert set(tm.last_paths.values()) <= {host_path, "fused_staged"}, \
+                            tm.last_paths
+                    n += 1
+            assert n > 10
+            c = next(c for c in CASES if c["type"] == t and c["op"] == op and c["npes"] == 3
+                     and c["nreduce"] == 4097 and c["tag"] == "grid")
+            check(c, run_case(tm, c, in_place=True))
+    finally:
+        L.osgpu_set_host_chunk_bytes(-1)
+        L.osgpu_set_stage_bytes(-1)
+        L.osgpu_finalize()
+
+
+@pytest.mark.parametrize("t,op", [("int", "sum"), ("double", "sum"), ("long", "and"),
+                                  ("float", "min"), ("complexd", "prod"), ("complexf", "sum"),
+                                  ("short", "prod"), ("longdouble", "prod"),
+                                  ("longdouble", "max"), ("double", "max"), ("float", "prod")])
+def test_host_fold_matches_golden(torch_cuda, t, op):
+    """The library's default for small HOST symmetric-heap calls (at most 64
+    KiB per PE): the host fold (shmem_reduce.cpp run_host_fold, host_fold.hip)
+    -- the reference's algorithm on each PE's thread with the kernels'
+    element ops compiled for the host.  Bit-exact on the golden cases (NaN
+    payloads, signed zeros, wrap-around, x87 long double included), in
+    place too; above the limit the same calls take the GPU (STAGED)."""
+    tm = team(device=False, host_fold=True)
+    lim = 64 << 10
+    n = nfold = 0
     for c in CASES:
         if c["type"] == t and c["op"] == op and c["nreduce"] <= 4097 and \
                 c["npes"] in (1, 2, 3, 8):
             check(c, run_case(tm, c))
+            s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
+            if c["nreduce"] > 0:
+                want = "host_fold" if c["nreduce"] * s <= lim else "staged"
+                assert set(tm.last_paths.values()) <= {want, "fused_staged"}, tm.last_paths
+                nfold += want == "host_fold"
             n += 1
-    assert n > 10
+    assert n > 10 and nfold > 5
     c = next(c for c in CASES if c["type"] == t and c["op"] == op and c["npes"] == 3
              and c["nreduce"] == 4097 and c["tag"] == "grid")
     check(c, run_case(tm, c, in_place=True))
-    osgpu.load().osgpu_finalize()
 
 
 @pytest.mark.parametrize("stage_copy", ["kout", "kernel", "dma"])
@@ -191,10 +230,10 @@ def test_host_staged_copy_modes(torch_cuda, stage_copy, pinned, monkeypatch):
     pinned bounce buffers' device view) and on heaps pinned with
     osgpu_host_register (the heap's own device view), 4 KiB chunks, odd
     lengths and offsets: bit-exact on the golden cases."""
-    monkeypatch.setenv("OSGPU_STAGE_BYTES", "4096")
-    monkeypatch.setenv("OSGPU_HOST_PATH", "staged")
-    monkeypatch.setenv("OSGPU_STAGE_COPY", stage_copy)
     L = osgpu.load()
+    L.osgpu_set_stage_bytes(4096)
+    L.osgpu_set_host_path(osgpu.HOST_STAGED)
+    L.osgpu_set_stage_copy(osgpu.STAGE_COPY[stage_copy])
     L.osgpu_finalize()
     tm = team(device=False)
     if pinned:
@@ -215,6 +254,9 @@ def test_host_staged_copy_modes(torch_cuda, stage_copy, pinned, monkeypatch):
         if pinned:
             L.osgpu_set_fused_max_bytes(-1)
             L.osgpu_host_unregister(ctypes.c_void_p(tm.base))
+        L.osgpu_set_stage_bytes(-1)
+        L.osgpu_set_host_path(-1)
+        L.osgpu_set_stage_copy(-1)
         L.osgpu_finalize()
 
 

@@ -15,7 +15,7 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc $FL $X -c longdouble.hip -o $d/longdouble.o &
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
-      $d/combine.o $d/team.o $d/fused.o verify.o $d/longdouble.o copy.o runtime.o heap.o \
+      $d/combine.o $d/team.o $d/fused.o verify.o $d/longdouble.o copy.o host_fold.o runtime.o heap.o \
       shmem_reduce.o shmem_collect.o -lrccl -ldl -lpthread
   rm -f $d/*.o
   echo "built tools/ab/$name"

@@ -123,10 +123,9 @@ def main():
             rec["device_frac_of_8TBps"] = moved(kind, P, nb) / t / HBM_PEAK
         if "host" not in skip:
             for hp in ("staged", "getmem"):
-                os.environ["OSGPU_HOST_PATH"] = hp
-                t = api_time(kind, P, nb, max(3, a.reps // 3), False)
+                with osgpu.host_path(hp):
+                    t = api_time(kind, P, nb, max(3, a.reps // 3), False)
                 rec[f"host_{hp}_ms"] = t * 1e3
-            del os.environ["OSGPU_HOST_PATH"]
         if "cpu" not in skip:
             t = OC.cpu_baseline(kind, P, nb, root=1, reps=5)
             rec["cpu_reference_loop_ms"] = t * 1e3
