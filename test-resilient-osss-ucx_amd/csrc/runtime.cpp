@@ -947,15 +947,18 @@ int host_path()
     return g_host_path < 0 ? env : g_host_path;
 }
 
-// Per-PE byte limit of the host fold (host_fold.hip) on the automatic host
-// path: OSGPU_HOST_FOLD_MAX_BYTES, default 64 KiB (16 Ki ints; the measured
-// crossovers: DESIGN.md 10); 0 turns it off.
+// Limit of the host fold (host_fold.hip) on the automatic host path, on the
+// bytes each PE pulls from its peers, (PE_size - 1) * nreduce * size:
+// OSGPU_HOST_FOLD_MAX_BYTES, default 256 KiB (2 PEs: 64 Ki ints, where the
+// fold took 10 us against 41 us for the fused staged launch and 15 us for
+// the fused launch on device heaps, profiles/r06_bench_run2.log small_call);
+// 0 turns it off.
 long long g_host_fold_max = -1;
 
 size_t host_fold_max_bytes()
 {
     static const long long env = [] {
-        const long long v = env_ll("OSGPU_HOST_FOLD_MAX_BYTES", 64LL << 10);
+        const long long v = env_ll("OSGPU_HOST_FOLD_MAX_BYTES", 256LL << 10);
         return v < 0 ? 0 : v;
     }();
     std::lock_guard<std::mutex> lk(g_mu);

@@ -689,8 +689,8 @@ void run_host(const Call &c)
     }
 }
 
-// Small calls on HOST symmetric-heap memory (at most host_fold_max_bytes()
-// per PE, automatic host path): the reference's algorithm on this PE's
+// Small calls on HOST symmetric-heap memory (each PE pulling at most
+// host_fold_max_bytes() from its peers, automatic host path): the reference's algorithm on this PE's
 // thread with the kernels' element ops compiled for the host (host_fold.hip)
 // -- the source copied into the target, barrier (src/reductions.c:82), every
 // other PE's whole source pulled with ONE shmem_getmem (the reference pulls
@@ -751,7 +751,7 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
             fatal(name, "no GPU visible: the combine runs only on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
         // a size every member shares: all of them take the same path
-        if (hp == OSGPU_HOST_AUTO && c.nbytes <= host_fold_max_bytes() &&
+        if (hp == OSGPU_HOST_AUTO && (size_t) (c.PE_size - 1) * c.nbytes <= host_fold_max_bytes() &&
             osgpu::host_fold_supported(type, op)) {
             run_host_fold(c);
             return;

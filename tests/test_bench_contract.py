@@ -233,14 +233,15 @@ def test_trial_labels():
     """A slow trial is a box transient when the canary around it was slow,
     a placement when the canary was normal."""
     import bench
-    tr = [{"frac": 0.78, "copy_frac": 0.80, "canary": [0.80, 0.80]},
-          {"frac": 0.30, "copy_frac": 0.80, "canary": [0.31, 0.79]},
-          {"frac": 0.79, "copy_frac": 0.25, "canary": [0.80, 0.81]},
-          {"frac": 0.80, "copy_frac": 0.81, "canary": [0.80, 0.79]}]
+    tr = [{"frac": 0.78, "copy_frac": 0.80, "canary": [0.80, 0.80], "spread": [1.0, 1.0]},
+          {"frac": 0.30, "copy_frac": 0.80, "canary": [0.31, 0.79], "spread": [1.0, 1.0]},
+          {"frac": 0.79, "copy_frac": 0.25, "canary": [0.80, 0.81], "spread": [1.0, 1.02]},
+          {"frac": 0.80, "copy_frac": 0.81, "canary": [0.80, 0.79], "spread": [1.0, 1.0]},
+          {"frac": 0.79, "copy_frac": 0.20, "canary": [0.80, 0.79], "spread": [1.0, 4.1]}]
     by = {"4": {"trials": tr}, "canary": {"median": 0.8}}
     counts = bench.label_trials(by, 0.8)
-    assert [t["label"] for t in tr] == ["ok", "transient", "placement", "ok"]
-    assert counts == {"ok": 2, "transient": 1, "placement": 1}
+    assert [t["label"] for t in tr] == ["ok", "transient", "placement", "ok", "transient"]
+    assert counts == {"ok": 2, "transient": 2, "placement": 1}
 
 
 def test_compile_time_knobs_bounded():

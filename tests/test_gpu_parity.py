@@ -197,14 +197,14 @@ def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
                                   ("short", "prod"), ("longdouble", "prod"),
                                   ("longdouble", "max"), ("double", "max"), ("float", "prod")])
 def test_host_fold_matches_golden(torch_cuda, t, op):
-    """The library's default for small HOST symmetric-heap calls (at most 64
-    KiB per PE): the host fold (shmem_reduce.cpp run_host_fold, host_fold.hip)
+    """The library's default for small HOST symmetric-heap calls (each PE
+    pulling at most 256 KiB from its peers): the host fold (shmem_reduce.cpp run_host_fold, host_fold.hip)
     -- the reference's algorithm on each PE's thread with the kernels'
     element ops compiled for the host.  Bit-exact on the golden cases (NaN
     payloads, signed zeros, wrap-around, x87 long double included), in
     place too; above the limit the same calls take the GPU (STAGED)."""
     tm = team(device=False, host_fold=True)
-    lim = 64 << 10
+    lim = 256 << 10   # on (PE_size - 1) * nreduce * size
     n = nfold = 0
     for c in CASES:
         if c["type"] == t and c["op"] == op and c["nreduce"] <= 4097 and \
@@ -212,7 +212,7 @@ def test_host_fold_matches_golden(torch_cuda, t, op):
             check(c, run_case(tm, c))
             s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
             if c["nreduce"] > 0:
-                want = "host_fold" if c["nreduce"] * s <= lim else "staged"
+                want = "host_fold" if (c["PE_size"] - 1) * c["nreduce"] * s <= lim else "staged"
                 assert set(tm.last_paths.values()) <= {want, "fused_staged"}, tm.last_paths
                 nfold += want == "host_fold"
             n += 1

@@ -172,8 +172,8 @@ def test_host_staged_processes(tmp_path, world, monkeypatch):
     reference's own data placement.  STAGED: H2D -> exchange through the
     IPC-mapped staging buffers -> D2H (64 KiB chunks: many pipeline turns);
     GETMEM: peers' sources pulled through the runtime's getmem; fold: the
-    default automatic path, whose calls up to 64 KiB per PE are folded on
-    the host (shmem_reduce.cpp run_host_fold) -- bit-exact against the same
+    default automatic path, whose calls pulling at most 256 KiB per PE are
+    folded on the host (shmem_reduce.cpp run_host_fold) -- bit-exact against the same
     golden vectors."""
     import torch
     if not torch.cuda.is_available():
@@ -192,7 +192,7 @@ def test_host_staged_processes(tmp_path, world, monkeypatch):
             s = 16 if t == "longdouble" else np.dtype(O.NP_DTYPE[t]).itemsize
             small = fused == "-1" and t != "longdouble" and n * s <= (1 << 20)
             want = ("getmem" if hp == "getmem" else
-                    "host_fold" if hp == "fold" and n * s <= (64 << 10) else
+                    "host_fold" if hp == "fold" and (world - 1) * n * s <= (256 << 10) else
                     "fused_staged" if pinned == "1" and small else "staged")
             assert ran == want, (key, r, ran)
     _check_colls(res, "staged")
