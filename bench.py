@@ -2034,7 +2034,7 @@ def bench_multi(args):
             res["collectives"] = {"error": repr(e)[:300]}
 
     # ---- BASELINE config 1's shape across GPUs: fused one-launch path vs
-    # host barriers
+    # host barriers (DESIGN_HISTORY.md 10)
     if team_ok and not args.no_extra:
         state["phase"] = "small_calls"
         try:

@@ -4,7 +4,7 @@
 // memory, written over xGMI (or inside one GPU) by the kernel itself.
 //
 // Why: a small call on the host-barrier path costs a launch, a completion
-// wait and two host barriers (~25-30 us for 1 Ki ints); the
+// wait and two host barriers (~25-30 us for 1 Ki ints, DESIGN_HISTORY.md 5); the
 // compute is noise.  Here the host enqueues ONE kernel and waits once.
 //
 // Per active set every member PE owns a flag area (uncached device memory,

@@ -6,17 +6,19 @@
 // every other PE's source with a blocking 64-element shmem_getmem and fold it
 // through an indirect call per element, barrier).  For 1 Ki ints that loop
 // takes 4-7 us; the GPU paths cannot come below a kernel launch whose
-// completion the host sees (6.4 us for an empty kernel) plus
-// the PCIe legs: the fused one-launch staged path takes 15-17 us.  So below
-// host_fold_max_bytes() per PE (shmem_reduce.cpp) a host-heap call is folded
-// here: one shmem_getmem per peer of its whole source, and a direct
-// (inlined, not indirect) fold in the reference's per-PE order.
+// completion the host sees (6.4 us for an empty kernel, DESIGN_HISTORY.md
+// 10) plus the PCIe legs: the fused one-launch staged path takes 15-17 us.
+// So while a PE pulls at most host_fold_max_bytes() from its peers
+// (shmem_reduce.cpp run_host_fold) a host-heap call is folded here: one
+// shmem_getmem per peer of its whole source, and a direct (inlined, not
+// indirect) fold in the reference's per-PE order.
 //
 // The element ops are the SAME definitions the kernels use (elem_ops.hpp
 // functors, x87.hpp soft-float for long double), compiled for the host: the
-// results are bit-identical to the GPU paths' (tests/test_gpu_host_fold.py
-// checks both against the golden vectors), not merely to the host compiler's
-// view of the C operators.
+// results are bit-identical to the GPU paths' (tests/test_gpu_parity.py
+// test_host_fold_matches_golden and tests/test_multiproc.py
+// test_host_staged_processes check both against the golden vectors), not
+// merely to the host compiler's view of the C operators.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>

@@ -877,7 +877,7 @@ StageSet *stage_setup(const Coll &c)
     if (procs_here > 1) {
         // PE processes sharing this GPU also share its hardware queue slots
         // (HIP gives each process up to 4; past 16 on the GPU its scheduler
-        // time-slices them in milliseconds) and its PCIe link:
+        // time-slices them in milliseconds, DESIGN_HISTORY.md 10) and its PCIe link:
         // the staging copies and folds go on the PE's own stream, in order,
         // so this process holds no queue beyond it
         S.st_in = S.st_out = S.st_c = pe_ctx(c.name, c.me).stream;

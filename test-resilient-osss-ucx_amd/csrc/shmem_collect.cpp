@@ -581,7 +581,7 @@ void collective(const char *name, Kind kind, size_t esz, void *target, const voi
         // PE's PCIe link; that beats the runtime's memcpy only for large
         // calls and only when every member has a GPU (and a link) of its
         // own -- PEs sharing a GPU share its link (tools/coll_bench.py,
-        // DESIGN.md 9).  Small calls (the fused limit, a size every member
+        // DESIGN_HISTORY.md 9).  Small calls (the fused limit, a size every member
         // shares) stay on the runtime's getmem: no GPU round trip beats a
         // same-node copy of a few KiB (1 Ki ints: 1.6 us vs 14 us for the
         // one-launch staged form, profiles/r01_mp_latency_host_coll.jsonl).

@@ -698,7 +698,7 @@ void run_host(const Call &c)
 // barrier (:113), the temporary target copied back on overlap (:114-119).
 // No GPU round trip: below this size the fastest GPU form (one fused launch
 // reading and writing the host heap over PCIe) costs more than the whole
-// loop (DESIGN.md 10).
+// loop (DESIGN.md 5.6).
 void run_host_fold(const Call &c)
 {
     t_last_path = OSGPU_RAN_HOST_FOLD;
