@@ -1545,12 +1545,18 @@ int osgpu_combine(int type, int op, void *target, const void *const *srcs, int n
 int osgpu_team_combine(int type, int op, int P, void *const *dsts, const void *const *srcs,
                        size_t nelems, void *hip_stream)
 {
+    return osgpu_team_combine_shape(type, op, P, dsts, srcs, nelems, hip_stream, 0);
+}
+
+int osgpu_team_combine_shape(int type, int op, int P, void *const *dsts, const void *const *srcs,
+                             size_t nelems, void *hip_stream, int remote)
+{
     if (!has_op(type, op) || P < 2 || P > osgpu::kMaxTeam || !dsts || !srcs) {
         set_err("osgpu_team_combine: bad arguments");
         return OSGPU_EINVAL;
     }
     hipStream_t st = hip_stream ? (hipStream_t) hip_stream : thread_stream("osgpu_team_combine");
-    hipError_t e = osgpu::launch_team(type, op, P, dsts, srcs, nelems, st);
+    hipError_t e = osgpu::launch_team(type, op, P, dsts, srcs, nelems, st, remote != 0);
     if (e != hipSuccess) {
         set_err("osgpu_team_combine: %s", hipGetErrorString(e));
         return OSGPU_EHIP;

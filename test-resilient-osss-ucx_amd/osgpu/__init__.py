@@ -134,6 +134,7 @@ def load() -> ctypes.CDLL:
     L.osgpu_combine.argtypes = [i, i, vp, vp, i, sz, vp]
     L.osgpu_copy.argtypes = [vp, vp, vp, i, vp]
     L.osgpu_team_combine.argtypes = [i, i, i, vp, vp, sz, vp]
+    L.osgpu_team_combine_shape.argtypes = [i, i, i, vp, vp, sz, vp, i]
     L.osgpu_build_id.restype = ctypes.c_char_p
     L.osgpu_has_op.argtypes = [i, i]
     L.osgpu_type_size.argtypes = [i]

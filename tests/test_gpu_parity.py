@@ -537,6 +537,46 @@ def test_team_combine_launcher(torch_cuda, t, op, P, shift):
         assert (outs[q][off + n * s:].cpu().numpy() == 0x5A).all()
 
 
+REMOTE_CASES = [(t, op, P) for P in (2, 5, 8)
+                for t, op in (("double", "sum"), ("float", "prod"), ("double", "min"),
+                              ("float", "max"), ("int", "sum"), ("long", "xor"),
+                              ("short", "prod"), ("complexf", "sum"), ("complexd", "prod"))]
+
+
+@pytest.mark.parametrize("t,op,P", REMOTE_CASES)
+def test_team_remote_shapes_match_golden(torch_cuda, t, op, P):
+    """The team kernel's REMOTE launch shapes (team.hip TeamShape<..., true>:
+    the register form at 2 members, rounds of 2 vectors at 5-8 -- what a
+    call whose members' heaps sit on other GPUs launches) run on
+    one GPU through osgpu_team_combine_shape: every member's output
+    bit-exact against the oracle on edge-value inputs (NaN payloads, ±0,
+    infinities, wrap-around), with a scalar head and tail."""
+    s = np.dtype(O.NP_DTYPE[t]).itemsize
+    n = 50_003
+    src = O.team_inputs(t, P, n, 0x3E70 + P, "edge")
+    want = O.to_all(t, op, src)
+    nb = n * s + 64
+    dev = torch_cuda.device("cuda:0")
+    ins = [torch_cuda.empty(nb, dtype=torch_cuda.uint8, device=dev) for _ in range(P)]
+    outs = [torch_cuda.full((nb,), 0x5A, dtype=torch_cuda.uint8, device=dev) for _ in range(P)]
+    off = s
+    for p in range(P):
+        raw = np.ascontiguousarray(src[p]).view(np.uint8).reshape(-1)
+        ins[p][off:off + raw.size].copy_(torch_cuda.from_numpy(raw.copy()).to(dev))
+    S = (ctypes.c_void_p * P)(*[x.data_ptr() + off for x in ins])
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() + off for x in outs])
+    torch_cuda.cuda.synchronize()
+    L = osgpu.load()
+    assert L.osgpu_team_combine_shape(osgpu.TYPES.index(t), osgpu.OPS.index(op), P, D, S, n,
+                                      None, 1) == 0
+    torch_cuda.cuda.synchronize()
+    for q in range(P):
+        got = outs[q][off:off + n * s].cpu().numpy()
+        assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (t, op, P, q)
+        assert (outs[q][:off].cpu().numpy() == 0x5A).all()
+        assert (outs[q][off + n * s:].cpu().numpy() == 0x5A).all()
+
+
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
 @pytest.mark.parametrize("sign", [0, 1])
 def test_longdouble_same_sign_sums(torch_cuda, P, sign):
