@@ -140,6 +140,8 @@ def fit_line(res, detail_path=None, cap=LINE_CAP):
             res = dict(res, detail=f"not written: {e}"[:200])
     line = {}
     for k, v in res.items():
+        if k in DETAIL_ONLY:
+            continue
         try:
             line[k] = _shrink(SUMMARIZERS[k](v) if k in SUMMARIZERS and isinstance(v, dict) else v, k)
         except Exception as e:  # a summary must never cost the line
