@@ -751,7 +751,8 @@ void to_all(const char *name, int type, int op, void *target, void *source, int 
             fatal(name, "no GPU visible: the combine runs only on the GPU");
         if (!c.ops.getmem) fatal(name, "host-memory arguments need shmem_getmem");
         // a size every member shares: all of them take the same path
-        if (hp == OSGPU_HOST_AUTO && (size_t) (c.PE_size - 1) * c.nbytes <= host_fold_max_bytes() &&
+        const size_t fold_lim = host_fold_max_bytes();  // 0: off
+        if (hp == OSGPU_HOST_AUTO && fold_lim > 0 && (size_t) (c.PE_size - 1) * c.nbytes <= fold_lim &&
             osgpu::host_fold_supported(type, op)) {
             run_host_fold(c);
             return;

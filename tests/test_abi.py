@@ -281,3 +281,33 @@ def test_test_hook_refused_in_production(lib, monkeypatch):
     lib.osgpu_test_preflight_fault.argtypes = [ctypes.c_int, ctypes.c_int]
     assert lib.osgpu_test_preflight_fault(0, 1) != 0
     assert b"test hooks are off" in lib.osgpu_last_error()
+
+
+def test_product_never_references_the_oracle():
+    """nothing under the product (csrc/, osgpu/, the
+    public header) includes, links, loads or calls oracle/ -- outside
+    comments the word does not appear, and the built library has no
+    dependency on liboracle / libref_ops."""
+    import glob
+    import re
+    pkg = os.path.join(ROOT, "test-resilient-osss-ucx_amd")
+    files = (glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.cpp"))
+             + glob.glob(os.path.join(pkg, "csrc", "*.hpp")) + glob.glob(os.path.join(pkg, "csrc", "Makefile"))
+             + glob.glob(os.path.join(pkg, "osgpu", "*.py"))
+             + [os.path.join(ROOT, "include", "osgpu_reduce.h")])
+    bad = []
+    for f in files:
+        src = open(f).read()
+        if f.endswith(".py") or f.endswith("Makefile"):
+            code = re.sub(r"#.*", "", src)
+            code = re.sub(r'"""(.|\n)*?"""', "", code)
+        else:
+            code = re.sub(r"/\*(.|\n)*?\*/", "", src)
+            code = re.sub(r"//.*", "", code)
+        if re.search(r"oracle|ref_ops", code, re.IGNORECASE):
+            bad.append(os.path.relpath(f, ROOT))
+    assert not bad, bad
+    so = os.path.join(pkg, "libosgpu_reduce.so")
+    if os.path.exists(so):
+        out = subprocess.run(["readelf", "-d", so], capture_output=True, text=True).stdout
+        assert "oracle" not in out and "ref_ops" not in out

@@ -266,8 +266,9 @@ def test_staged_copy_streams_survive_extra_streams(torch_cuda):
     H2D and D2H copy streams still come from different priority pools, and
     a 64 Mi-double pinned STAGED call keeps both directions moving at once:
     more than 36 GB/s each way (27.7 when they shared a queue and took
-    turns), unless the GPU's DMA engine is in its low power state (then
-    its D2H alone is below 40 GB/s and the rate is not asserted)."""
+    turns), unless the GPU's DMA engine was in its low power state before
+    or after the timed calls (then its D2H alone is below 40 GB/s and the
+    rate is only reported).  The hard assertion is the priorities'."""
     import torch
     import bench
     side = torch.cuda.Stream()
@@ -287,7 +288,12 @@ def test_staged_copy_streams_survive_extra_streams(torch_cuda):
     pi, po = ctypes.c_int(), ctypes.c_int()
     assert L.osgpu_copy_stream_info(dev, ctypes.byref(pi), ctypes.byref(po)) == 0
     assert pi.value != po.value, (pi.value, po.value)
-    if not res["dma_state"]["low_state"]:
+    # the rate is reported, and asserted only when the DMA engine was in its
+    # high power state both before and after the timed calls (ADVICE r05:
+    # a state drop during them must not fail a test about stream priorities)
+    print("pinned STAGED each way GB/s", res["pinned"]["pcie_GBs_each_way"],
+          "dma before/after", res["dma_state"], res["dma_state_after"])
+    if not res["dma_state"]["low_state"] and not res["dma_state_after"]["low_state"]:
         assert res["pinned"]["pcie_GBs_each_way"] > 36, res
     del side
 

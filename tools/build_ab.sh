@@ -1,14 +1,21 @@
 #!/bin/bash
 # Build libosgpu_reduce variants into tools/ab/<name>/ for one-lease A/B runs
 # (tools/ab is gpurun-ignored by default: the calling script lists it).
+# Builds in a scratch copy of csrc/, so the in-tree library and objects are
+# never touched (a GPU call may be snapshotting the tree meanwhile).
 #   tools/build_ab.sh name "-DFLAG=1 -DOTHER=2" [name2 "flags2" ...]
 set -e
-cd "$(dirname "$0")/../test-resilient-osss-ucx_amd/csrc"
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+W=$(mktemp -d /tmp/osgpu_ab.XXXXXX)
+mkdir -p "$W/test-resilient-osss-ucx_amd" "$W/include"
+cp -r "$ROOT/test-resilient-osss-ucx_amd/csrc" "$W/test-resilient-osss-ucx_amd/"
+cp "$ROOT/include/osgpu_reduce.h" "$W/include/"
+cd "$W/test-resilient-osss-ucx_amd/csrc"
 make -s -j8
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math"
 while [ $# -ge 2 ]; do
   name=$1; X=$2; shift 2
-  d=../../tools/ab/$name; mkdir -p $d
+  d=$ROOT/tools/ab/$name; mkdir -p $d
   /opt/rocm/bin/hipcc $FL $X -c combine.hip -o $d/combine.o &
   /opt/rocm/bin/hipcc $FL $X -c team.hip -o $d/team.o &
   /opt/rocm/bin/hipcc $FL $X -c fused.hip -o $d/fused.o &
@@ -20,3 +27,4 @@ while [ $# -ge 2 ]; do
   rm -f $d/*.o
   echo "built tools/ab/$name"
 done
+rm -rf "$W"
