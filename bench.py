@@ -85,7 +85,7 @@ DROP_ORDER = ("host_staged_in_torch_process", "cpu_baseline_configs", "traffic_l
               "api", "collectives", "longdouble_team_8_members", "config3_long_bitwise_256MiB",
               "north_star_double_sum_128Mi", "config5_host_staged", "host_staged",
               "roofline_call", "small_call", "team_by_members", "local_fold_no_exchange",
-              "team_push", "xgmi_probe", "small_calls", "config5",
+              "team_shapes_ab", "team_push", "xgmi_probe", "small_calls", "config5",
               "rccl_integer_auto", "launch", "config4", "rccl", "hbm_aggregate")
 
 
@@ -1490,6 +1490,40 @@ def _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes, reps=5):
     return out
 
 
+def _team_shapes_ab(L, osgpu, torch, dist, rank, world, bases, n, tgt, args, reps=5):
+    """The team kernel's local and remote launch shapes on the real heaps:
+    rank g launches shard g of the double sum over every member's source and
+    target (peer HBM over xGMI when the ranks have GPUs of their own) with
+    osgpu_team_combine_shape(shape), every rank at once, timed between
+    barriers; max over ranks.  The targets of the two shapes must agree bit
+    for bit (a position-weighted hash of every PE's whole target)."""
+    lo, hi = osgpu.shard_range(n, world, rank, 8)
+    m = hi - lo
+    S = (ctypes.c_void_p * world)(*[bases[(pe, 0)] + lo * 8 for pe in range(world)])
+    D = (ctypes.c_void_p * world)(*[bases[(pe, 1)] + lo * 8 for pe in range(world)])
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    out = {"note": "kernel only: shard of the double sum per rank, all ranks at once",
+           "members": world, "shard_elems": m}
+    hashes = {}
+    for name, shape in (("local_shapes", 0), ("remote_shapes", 1)):
+        def step():
+            if m > 0:
+                assert L.osgpu_team_combine_shape(5, 0, world, D, S, m, sp, shape) == 0
+            st.synchronize()
+
+        t = _timed(step, reps, 2, dist, torch)
+        dist.barrier()   # every shard of every target written
+        hashes[name] = osgpu.checksum("double", osgpu.CK_HASH, tgt.data_ptr(), n)
+        B = 2 * world * n * 8      # the whole team's bytes per step
+        out[name] = {"ms": t / reps * 1e3, "hbm_GBs_all_gpus": reps * B / t / 1e9,
+                     "xgmi_in_GBs_per_gpu": reps * 2 * (world - 1) * (n * 8 // world) / t / 1e9}
+    out["remote_over_local"] = out["local_shapes"]["ms"] / out["remote_shapes"]["ms"]
+    out["identical_targets_all_ranks"] = _agree(
+        dist, world, hashes["local_shapes"] == hashes["remote_shapes"])
+    return out
+
+
 def _multi_small(L, osgpu, torch, dist, rank, world, hsrc, htgt, PES, reps=200, flags_ok=True):
     """BASELINE config 1's shape with one PE per GPU: shmem_int_sum_to_all,
     nreduce = 1 Ki, device heaps over xGMI -- host barriers vs the fused
@@ -1841,6 +1875,21 @@ def bench_multi(args):
             L.osgpu_set_team_exchange(-1)
     else:
         res["team_error"] = "HIP IPC export/import of the device heaps failed on some rank"
+
+    # ---- the team kernel's two launch shapes over the same heaps (ADVICE
+    # r05): every rank launches its shard of the double sum with the local
+    # shapes (one-GPU A/Bs: LDS form at 2 members, rounds of 4 at 5-8) and
+    # with the remote ones (register form at 2, rounds of 2) that the TEAM
+    # path picks when members sit on other GPUs -- kernel only, all ranks at
+    # once, max over ranks; bit-identical outputs checked
+    if team_ok and not args.no_extra:
+        state["phase"] = "team_shapes"
+        try:
+            res["team_shapes_ab"] = _team_shapes_ab(L, osgpu, torch, dist, rank, world, bases,
+                                                    n, tgt, args)
+            _log(rank, "team shapes done")
+        except Exception as e:
+            res["team_shapes_ab"] = {"error": repr(e)[:300]}
 
     # ---- the local fold alone on every GPU at once (config 2's kernel: my
     # source + a second resident array, K = 2, NO exchange).  This is not a
