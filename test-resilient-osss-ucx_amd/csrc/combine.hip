@@ -170,9 +170,11 @@ constexpr int kCombineLdsMaxK = 8;
 #define OSGPU_COMBINE_LDS_U2 2  // vectors per lane per input at K = 2 (the headline kernel)
 #endif
 constexpr int kCombineLdsU = 4;  // ... at K = 3 .. 8
-#ifndef OSGPU_COMBINE_GLDS
-#define OSGPU_COMBINE_GLDS 0  // round-6 A/B: LDS-DMA staging of the tile
-#endif
+// (Round 6, in one process on the same arrays, 6 allocations each,
+// profiles/r06_combine_glds_ab.jsonl: the tile staged by LDS-DMA --
+// global_load_lds_dwordx4, no VGPR round trip -- 1.005x at U = 2 (min
+// 0.997x), 0.985x at U = 4, 0.975x at U = 8; register staging at U = 4
+// 0.979x.  Within noise at best: the register staging ships.)
 
 template <typename T, int OP, int K, int U>
 __global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K> in, size_t nvec,
@@ -194,17 +196,6 @@ __global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K
     for (int k = 1; k < K; k++)
         if (w == k) pw = in.p[k];
     const u32x4 *src = reinterpret_cast<const u32x4 *>(pw + head);
-#if OSGPU_COMBINE_GLDS
-    if (whole) {  // LDS-DMA: the tile straight into LDS, no VGPR round trip
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            __builtin_amdgcn_global_load_lds(
-                (__attribute__((address_space(1))) void *) (src + base + u * 64 + lane),
-                (__attribute__((address_space(3))) void *) &tile[w][u * 64], 16, 0, 2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else
-#endif
-    {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -212,7 +203,6 @@ __global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K
             v[u] = __builtin_nontemporal_load(src + base + u * 64 + lane);
 #pragma unroll
     for (int u = 0; u < U; u++) tile[w][u * 64 + lane] = v[u];
-    }
     __syncthreads();
     u32x4 *dst = reinterpret_cast<u32x4 *>(out + head);
     for (int j = (int) threadIdx.x; j < V; j += 64 * K) {

@@ -70,6 +70,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
     multi8_self) step multi8_self 900 python bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     multi4_s) step multi4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 200 ;;
+    proffull) step proffull 900 rocprofv3 --kernel-trace --stats -d gpurun_out/proffull -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof3) step prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 20 --warmup 5 ;;
     pmc3)  step pmc3f 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3f -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
            step pmc3w 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc3w -o run --output-format csv -- python3 bench.py --no-live-pmc --no-cpu-baseline --no-api --steps 5 --warmup 2 &&
