@@ -68,6 +68,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     tuneteam) step tuneteam 400 ./tools/tune_team ;;
     teamlayouts) step teamlayouts 400 ./tools/tune_team $((64<<20)) 20 6 layouts ;;
     teamoff) step teamoff 300 python -u tools/team_offsets.py ;;
+    multi8_small) step multi8_small 600 python bench.py --gpus 8 --steps 3 --warmup 1 --nreduce $((16<<20)) --c4-nreduce $((64<<20)) --c5-nreduce $((16<<20)) --deadline 500 ;;
     multi8_self) step multi8_self 900 python bench.py --gpus 8 --steps 5 --warmup 2 --deadline 800 ;;
     multi4_s) step multi4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce $((4<<20)) --c4-nreduce $((8<<20)) --c5-nreduce $((4<<20)) --deadline 200 ;;
     proffull) step proffull 900 rocprofv3 --kernel-trace --stats -d gpurun_out/proffull -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
