@@ -70,7 +70,7 @@ METRIC = "GiB/s device-resident shmem_double_sum_to_all combine + %HBM peak, 1/2
 # summary (min / median / max, no address lists) of each side measurement.
 # --------------------------------------------------------------------------
 
-LINE_CAP = 8192
+LINE_CAP = 7168  # under the driver's 8 KiB stdout tail with room to spare
 # keys whose values stay in the detail file only (anywhere in the tree)
 DETAIL_ONLY = frozenset((
     "addresses", "placements", "sweep", "heap_preflight", "ranks", "note", "how", "what",
@@ -122,9 +122,41 @@ def _sum_torch_staged(v):
             for k in ("pinned", "pageable", "error") if k in v}
 
 
+def _sum_team(v):
+    out = {}
+    for P, rec in v.items():
+        if not isinstance(rec, dict) or "trials" not in rec:
+            out[P] = rec
+            continue
+        r = {k: rec[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us", "traffic",
+                                 "copy_frac", "frac_of_copy_ceiling", "frac_min", "frac_median",
+                                 "frac_max", "frac_of_copy_ceiling_min",
+                                 "frac_of_copy_ceiling_median", "frac_of_copy_ceiling_max",
+                                 "canary_min", "canary_median", "bit_exact_sample") if k in rec}
+        r["trials"] = [{"frac": t["frac"], "copy_frac": t["copy_frac"], "canary": t["canary"],
+                        "label": t.get("label")} for t in rec["trials"]]
+        oa = rec.get("one_allocation_heaps_layout") or {}
+        r["one_allocation_heaps_of_copy"] = oa.get("frac_of_copy_ceiling")
+        out[P] = r
+    return out
+
+
+def _sum_small(v):
+    keys = ("fused_team", "team", "host_fused_staged", "host_staged", "host_fold")
+    out = {k + "_us": v.get(k + "_us_timed_in_c", v.get(k + "_us")) for k in keys}
+    out["timed"] = "in C between the runtime's barriers, median"
+    out["all_correct"] = all(v.get(k + "_correct", False) for k in keys)
+    for k in ("cpu_reference_loop_us", "default_path_us", "default_path", "crossover_elements",
+              "slower_than_reference_loop", "ratio_to_reference_loop", "error"):
+        if k in v:
+            out[k] = v[k]
+    return out
+
+
 # top-level side measurements given a purpose-made summary in the line
 SUMMARIZERS = {"cpu_baseline_configs": _sum_cpu_configs,
-               "host_staged_in_torch_process": _sum_torch_staged}
+               "host_staged_in_torch_process": _sum_torch_staged,
+               "team_by_members": _sum_team, "small_call": _sum_small}
 
 
 def fit_line(res, detail_path=None, cap=LINE_CAP):
@@ -297,18 +329,16 @@ def cpu_baseline(n):
     sec = O.cpu_baseline("double", "sum", src, reps=reps, pin=True, ref_ops=ref)
     wall = time.time() - t0
     B = 2 * 3 * n * 8  # two PE results, each (K+1)*n*8
-    ops = ("the reference's compiled shmemu_sum_double_func (src/shmemu/miscops.c built "
-           "unmodified into oracle/_ref) called by value through a pointer as "
-           "src/reductions.c:95-96 does" if ref else "the restated element op (oracle/_ref absent)")
+    ops = ("the reference's own shmemu_sum_double_func (miscops.c compiled unmodified into "
+           "oracle/_ref) through a pointer as src/reductions.c:95-96" if ref
+           else "the restated element op (oracle/_ref absent)")
     out = {"value": B / sec / GIB, "unit": "GiB/s", "cores": 2, "kind": "port",
            "element_ops": "reference" if ref else "restatement",
-           "sample": (f"src/reductions.c:79-113 loop shape restated in oracle/oracle_reduce.c "
-                      f"(copy, barrier, 64-element memcpy getmem chunks, barrier) with {ops}; "
-                      f"double sum, "
-                      f"2 PEs (pthreads pinned to the first 2 CPUs this process may use), nreduce={n}, median of "
-                      f"{reps} after 1 warm-up ({sec*1e3:.1f} ms/call, {wall:.1f} s total); "
-                      f"bytes = 2 PE results x 3*n*8; host nproc={os.cpu_count()}, CPUs this "
-                      f"process may use {len(os.sched_getaffinity(0))}")}
+           "sample": (f"src/reductions.c:79-113 loop restated (oracle/oracle_reduce.c: copy, "
+                      f"barrier, 64-element getmem chunks, barrier) calling {ops}; double sum, "
+                      f"2 PEs = 2 pinned pthreads, nreduce={n}, median of {reps} after 1 warm-up "
+                      f"({sec*1e3:.1f} ms/call, {wall:.1f} s); bytes = 2 x 3*n*8; host "
+                      f"nproc={os.cpu_count()}, usable CPUs {len(os.sched_getaffinity(0))}")}
     # the same loop with every PE's elements split over 8 threads: 16 cores,
     # this box's CPU share (a one-PE-per-core reference uses 2 for 2 PEs)
     tpp = 8

@@ -226,7 +226,8 @@ emit()
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1 and len(lines[0].encode()) <= 8192
+    import bench
+    assert len(lines) == 1 and len(lines[0].encode()) <= bench.LINE_CAP
 
 
 def test_trial_labels():
