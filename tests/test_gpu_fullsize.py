@@ -7,7 +7,9 @@ Every member's target is checked bit for bit against the reference's fold
 order for that member (src/reductions.c:79-111: PE q starts from its own
 source, then PE 0, 1, ... skipping q), restated with PyTorch element-wise
 IEEE operations in that order (no contraction: one rounding per operation,
-the reference's SSE arithmetic for float/double).
+the reference's SSE arithmetic for float/double) at full size, and against
+the oracle (oracle/, pinned by the reference's compiled element ops) on a
+64 Ki-element sample.
 
 * config 4: double sum, nreduce = 1 Gi (8 GiB per array), 8 PEs
   (64 GiB of sources, 64 GiB of targets);
@@ -61,6 +63,24 @@ def _fold(torch, op, srcs, q):
     return acc
 
 
+def _oracle_sample(torch, t, op, srcs, got, n, nsamp=1 << 16, seed=77):
+    """The full-size targets against the ORACLE (oracle/, the restatement
+    pinned by the reference's compiled element ops) on a sample of indices:
+    every PE's sampled inputs folded by the oracle in that PE's order,
+    compared bit for bit with every target at those indices (VERDICT r05
+    weak 2: the PyTorch fold above is not the oracle)."""
+    import numpy as np
+    import oracle as O
+    g = torch.Generator(device="cuda:0").manual_seed(seed)
+    idx = torch.randint(0, n, (nsamp,), device="cuda:0", generator=g)
+    xs = [np.ascontiguousarray(x[idx].cpu().numpy()) for x in srcs]
+    want = O.to_all(t, op, xs)
+    for q in range(P):
+        g_ = got[q][idx].cpu().numpy()
+        assert np.array_equal(g_.view(np.uint8), np.ascontiguousarray(want[q]).view(np.uint8)), \
+            (t, op, q)
+
+
 def _need(torch, nbytes):
     torch.cuda.empty_cache()
     free, _ = torch.cuda.mem_get_info()
@@ -77,6 +97,7 @@ def test_config4_double_sum_1Gi_8_pes(torch_cuda):
             for _ in range(P)]
     dsts = [torch.empty(n, dtype=torch.float64, device="cuda:0") for _ in range(P)]
     _team(torch, "double", "sum", srcs, dsts, n)
+    _oracle_sample(torch, "double", "sum", srcs, dsts, n)
     for q in range(P):
         want = _fold(torch, "sum", srcs, q)
         assert torch.equal(dsts[q].view(torch.int64), want.view(torch.int64)), q
@@ -99,6 +120,7 @@ def test_config5_float_128Mi_8_pes(torch_cuda, op, lo, hi):
             for _ in range(P)]
     dsts = [torch.empty(n, dtype=torch.float32, device="cuda:0") for _ in range(P)]
     _team(torch, "float", op, srcs, dsts, n)
+    _oracle_sample(torch, "float", op, srcs, dsts, n)
     for q in range(P):
         want = _fold(torch, op, srcs, q)
         assert torch.equal(dsts[q].view(torch.int32), want.view(torch.int32)), (op, q)
@@ -138,6 +160,10 @@ def test_config5_host_staged_128Mi_8_pes(torch_cuda, pinned):
                 torch.from_numpy(tm.hbuf[a:a + nb].view(np.float32)).copy_(srcs[pe])
             tm.run("float", op, toff, 0, n)
             assert set(tm.last_paths.values()) == {"staged"}, tm.last_paths
+            gots = [torch.from_numpy(tm.hbuf[tm.hoff + q * tm.H + toff:][:nb].view(np.float32))
+                    .to("cuda:0") for q in range(P)]
+            _oracle_sample(torch, "float", op, srcs, gots, n, seed=78)
+            del gots
             for q in range(P):
                 a = tm.hoff + q * tm.H + toff
                 got = torch.from_numpy(tm.hbuf[a:a + nb].view(np.int32)).to("cuda:0")
