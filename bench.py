@@ -153,8 +153,46 @@ def _sum_small(v):
     return out
 
 
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _sum_ld(v):
+    out = _pick(v, ("kernel", "members", "error"))
+    out["bound"] = "valu"
+    for k in ("random_signs", "one_sign"):
+        if isinstance(v.get(k), dict):
+            out[k] = _pick(v[k], ("frac", "kernel_avg_us", "member0_equals_member1"))
+    return out
+
+
+def _sum_c3(v):
+    out = _pick(v, ("nreduce", "error"))
+    for k in ("and", "or", "xor"):
+        if isinstance(v.get(k), dict):
+            out[k] = _pick(v[k], ("frac_of_8TBs", "kernel_us", "bit_exact"))
+    return out
+
+
+def _sum_c5h(v):
+    out = _pick(v, ("pes", "nreduce", "error"))
+    for k in ("min", "max", "prod"):
+        if isinstance(v.get(k), dict):
+            out[k] = _pick(v[k], ("pcie_GBs_each_way", "correct_sample"))
+    return out
+
+
+def _sum_coll(v):
+    return {"copy_kernel_frac_of_8TBps": (v.get("copy_kernel") or {}).get("frac_of_8TBps"),
+            "fcollect64_device_GBps_all_pes": (v.get("fcollect64_device") or {}).get("GBps_all_pes"),
+            "fcollect64_host_staged_h2d_GBs": (v.get("fcollect64_host_staged") or {}).get("pcie_h2d_GBs"),
+            **_pick(v, ("error",))}
+
+
 # top-level side measurements given a purpose-made summary in the line
-SUMMARIZERS = {"cpu_baseline_configs": _sum_cpu_configs,
+SUMMARIZERS = {"longdouble_team_8_members": _sum_ld, "config3_long_bitwise_256MiB": _sum_c3,
+               "config5_host_staged": _sum_c5h, "collectives": _sum_coll,
+               "cpu_baseline_configs": _sum_cpu_configs,
                "host_staged_in_torch_process": _sum_torch_staged,
                "team_by_members": _sum_team, "small_call": _sum_small}
 
