@@ -174,7 +174,11 @@ constexpr int kCombineLdsU = 4;  // ... at K = 3 .. 8
 // profiles/r06_combine_glds_ab.jsonl: the tile staged by LDS-DMA --
 // global_load_lds_dwordx4, no VGPR round trip -- 1.005x at U = 2 (min
 // 0.997x), 0.985x at U = 4, 0.975x at U = 8; register staging at U = 4
-// 0.979x.  Within noise at best: the register staging ships.)
+// 0.979x.  Within noise at best: the register staging ships.  Several
+// tiles per workgroup, the next tile's loads in flight during this one's
+// fold (profiles/r06_combine_tpw_ab.jsonl): 2 tiles 0.979x, 4 tiles 0.912x,
+// 4 strided tiles 0.922x, 4 tiles of U = 1 0.993x -- one tile per
+// workgroup, a one-shot grid, ships.)
 
 template <typename T, int OP, int K, int U>
 __global__ __launch_bounds__(64 * K) void combine_lds_kernel(T *out, Inputs<T, K> in, size_t nvec,

@@ -16,11 +16,13 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math"
 while [ $# -ge 2 ]; do
   name=$1; X=$2; shift 2
   d=$ROOT/tools/ab/$name; mkdir -p $d
-  /opt/rocm/bin/hipcc $FL $X -c combine.hip -o $d/combine.o &
-  /opt/rocm/bin/hipcc $FL $X -c team.hip -o $d/team.o &
-  /opt/rocm/bin/hipcc $FL $X -c fused.hip -o $d/fused.o &
-  /opt/rocm/bin/hipcc $FL $X -c longdouble.hip -o $d/longdouble.o &
+  # AB_FILES: the sources the flags affect (default all four kernel files);
+  # the others are linked from the scratch build unchanged
+  for f in ${AB_FILES:-combine team fused longdouble}; do
+    /opt/rocm/bin/hipcc $FL $X -c $f.hip -o $d/$f.o &
+  done
   wait
+  for f in combine team fused longdouble; do [ -f $d/$f.o ] || cp $f.o $d/$f.o; done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libosgpu_reduce.so \
       $d/combine.o $d/team.o $d/fused.o verify.o $d/longdouble.o copy.o host_fold.o runtime.o heap.o \
       shmem_reduce.o shmem_collect.o -lrccl -ldl -lpthread
