@@ -192,17 +192,15 @@ def test_host_staged_matches_golden(torch_cuda, t, op, host_path, monkeypatch):
         L.osgpu_finalize()
 
 
-@pytest.mark.parametrize("t,op", [("int", "sum"), ("double", "sum"), ("long", "and"),
-                                  ("float", "min"), ("complexd", "prod"), ("complexf", "sum"),
-                                  ("short", "prod"), ("longdouble", "prod"),
-                                  ("longdouble", "max"), ("double", "max"), ("float", "prod")])
+@pytest.mark.parametrize("t,op", sorted({(c["type"], c["op"]) for c in CASES}))
 def test_host_fold_matches_golden(torch_cuda, t, op):
     """The library's default for small HOST symmetric-heap calls (each PE
     pulling at most 256 KiB from its peers): the host fold (shmem_reduce.cpp run_host_fold, host_fold.hip)
     -- the reference's algorithm on each PE's thread with the kernels'
     element ops compiled for the host.  Bit-exact on the golden cases (NaN
     payloads, signed zeros, wrap-around, x87 long double included), in
-    place too; above the limit the same calls take the GPU (STAGED)."""
+    place too; above the limit the same calls take the GPU (STAGED).  Every
+    one of the 44 (type, op) pairs."""
     tm = team(device=False, host_fold=True)
     lim = 256 << 10   # on (PE_size - 1) * nreduce * size
     n = nfold = 0
