@@ -1558,7 +1558,7 @@ def _xgmi_probe(L, torch, dist, rank, world, bases, seg_bytes, reps=5):
     return out
 
 
-def _team_shapes_ab(L, osgpu, torch, dist, rank, world, bases, n, tgt, args, reps=5):
+def _team_shapes_ab(L, osgpu, torch, dist, rank, world, bases, n, tgt, reps=5):
     """The team kernel's local and remote launch shapes on the real heaps:
     rank g launches shard g of the double sum over every member's source and
     target (peer HBM over xGMI when the ranks have GPUs of their own) with
@@ -1954,7 +1954,7 @@ def bench_multi(args):
         state["phase"] = "team_shapes"
         try:
             res["team_shapes_ab"] = _team_shapes_ab(L, osgpu, torch, dist, rank, world, bases,
-                                                    n, tgt, args)
+                                                    n, tgt)
             _log(rank, "team shapes done")
         except Exception as e:
             res["team_shapes_ab"] = {"error": repr(e)[:300]}
