@@ -46,7 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # team.hip OSGPU_TEAM_LDS_U: vectors per lane per tile of the LDS-staged team
 # kernel (its template argument, the rocprof name's last field), and the
 # member counts that kernel serves (OSGPU_TEAM_LDS_MIN_P, OSGPU_TEAM_LDS_MAX_P)
-TEAM_LDS_U = 2
+TEAM_LDS_U = 1
 TEAM_LDS_P = (2, 4)
 # the headline kernel: combine.hip's LDS-staged form at K = 2 inputs
 # (OSGPU_COMBINE_LDS_U2 = 2 vectors per lane), its rocprof / PMC key and label

@@ -90,14 +90,21 @@ constexpr int kTeamU4 = 4;
 #ifndef OSGPU_TEAM_LDS_MAX_P
 #define OSGPU_TEAM_LDS_MAX_P 4
 #endif
-// 16-B vectors per lane per LDS tile: U = 2 (2 KiB per member per workgroup)
-// 1.02-1.04x over U = 4 at 3-4 members (profiles/r05_team_p34_ab.jsonl).
-// Round 6 (profiles/r06_team_p4_ab.jsonl, 5 allocations each, 4 members):
-// U = 2 staged by LDS-DMA (global_load_lds_dwordx4) 0.998x of this form, U = 4
-// by LDS-DMA 0.967x, LDS-DMA without the nt bit 0.982x, the register form
-// 0.986x; this form ran 0.98 of the same-mix copy there.
+// 16-B vectors per lane per LDS tile: U = 1 (1 KiB per member per workgroup,
+// round 6).  In one process on the same allocations against U = 2
+// (tools/team_inproc_ab.py, profiles/r06_lds_u1_confirm_ab.jsonl: 6 (type,
+// op) pairs x 2-4 members x 4 allocations) every pair's median was faster:
+// 1.025x / 1.026x / 1.070x at 2 / 3 / 4 members overall (int xor and float
+// prod 1.09x at 4, complex double prod 1.05-1.09x), lifting the 4-member
+// kernel from 0.963 to 1.021 of the same-mix copy
+// (profiles/r06_team_lds_u1_ab.jsonl: 1.04x / 1.00x / 1.09x for double
+// sum).  The same form at 5-8 members is mixed -- 1.07x at 5 and 6 for
+// double sum, 0.97x at 7, 0.72x for complex double prod at 8 -- so 5-8 keep
+// the register form.  (Round 5 had U = 2 over U = 4, 1.02-1.04x,
+// r05_team_p34_ab.jsonl; LDS-DMA staging at 4 members 0.967-0.998x,
+// r06_team_p4_ab.jsonl.)  The combine keeps U = 2: U = 1 there ran 0.966x.
 #ifndef OSGPU_TEAM_LDS_U
-#define OSGPU_TEAM_LDS_U 2
+#define OSGPU_TEAM_LDS_U 1
 #endif
 
 // Launch shape per (T, OP, P): U vectors per input per lane in rounds of G.
