@@ -126,13 +126,13 @@ OSGPU_HD inline uint32_t ffbh(uint32_t x)
 #endif
 }
 
-// |a - b| of two values below 2^16 (one v_sad_u16)
-OSGPU_HD inline uint32_t absdiff15(uint32_t a, uint32_t b)
+// |a - b| + c of two values below 2^16 (one v_sad_u16)
+OSGPU_HD inline uint32_t absdiff15(uint32_t a, uint32_t b, uint32_t c = 0u)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_sad_u16(a, b, 0u);
+    return __builtin_amdgcn_sad_u16(a, b, c);
 #else
-    return a > b ? a - b : b - a;
+    return (a > b ? a - b : b - a) + c;
 #endif
 }
 
@@ -264,6 +264,115 @@ OSGPU_HD inline bool add_same_fast(XU a, XU b, XU *r)
     const uint32_t hh = __builtin_addc((uint32_t) (hi >> 32), 0u, w1, &wrap);
     *r = XU{((uint64_t) hh << 32) | h0, E, a.s};
     return d - 63u >= 3u && !wrap && E < kEmax;
+}
+
+// leading bits equal to the sign bit of a 32-bit word, ~0 when it is 0 or
+// ~0 (what v_ffbh_i32 returns)
+OSGPU_HD inline uint32_t ffbh_signed(uint32_t x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t f;
+    asm("v_ffbh_i32 %0, %1" : "=v"(f) : "v"(x));
+    return f;
+#else
+    const uint32_t y = (x >> 31) ? ~x : x;
+    return y ? (uint32_t) __builtin_clz(y) : ~0u;
+#endif
+}
+
+// add_fast for two NORMAL operands whose exponents differ by at most 30
+// (the caller checks nothing; false otherwise): the same exact-then-round
+// sum, two bits lower -- A = ma * 2^62, B = mb * 2^(62-d) -- which buys:
+//  * B's lowest word is zero (d <= 30), so the sum has three words, not
+//    four: word 0 of A + ~B + 1 is 0 with carry `diff`, and that carry
+//    lands in A's word 1 as an OR (ma << 30 has 30 zero bits);
+//  * B's alignment is one 32-bit left shift and one 64-bit right shift, no
+//    drop mask (gaps above 30 are flagged);
+//  * a valid S has bit 127 clear (an addition lies below 2^127, a
+//    subtraction of the smaller magnitude below 2^126), so the only
+//    negative S -- a tie of (exponent, top word) with the larger low word
+//    subtracted, S > -2^94 -- has a top word of all ones, and the SIGNED
+//    leading-bit count (~0 for 0 and for ~0) flags it through the exponent
+//    range test with the 32-bit cancellations: no tie compare;
+//  * the round's low word is zero: one 32-bit carry test.
+// 41 VALU per add against add_fast's 51, ~1070 issue cycles per round of 7
+// adds against ~1290 (tools/isa/count_ld_valu.sh).  false: gaps above 30, cancellations of 32 bits or more, negative S,
+// results outside the normal range, all ones rounded up.
+OSGPU_HD inline bool add_near(XU a, XU b, XU *r)
+{
+    const uint64_t ka = ((uint64_t) a.e << 32) | (uint32_t) (a.m >> 32);
+    const uint64_t kb = ((uint64_t) b.e << 32) | (uint32_t) (b.m >> 32);
+    const bool swap = kb > ka;
+    const uint64_t ma = swap ? b.m : a.m;
+    const uint64_t mb = swap ? a.m : b.m;
+    const uint32_t EA = a.e > b.e ? a.e : b.e;
+    const uint32_t d2 = absdiff15(a.e, b.e, 2u);  // d + 2
+    const uint32_t sign = swap ? b.s : a.s;
+    // B = mb * 2^(62-d) = (mb << (30-d)) * 2^32: word 1 and words 2..3
+    // (30 - d = 32 - d2 under the shift's 5-bit mask)
+    unsigned far;  // d2 > 32: a gap above 30, flagged
+    const uint32_t b1 = (uint32_t) mb << (__builtin_subc(32u, d2, 0u, &far) & 31);
+    const uint64_t bh = mb >> (d2 & 63);
+    const uint64_t ah = ma >> 2;
+    const uint32_t diff = a.s ^ b.s;
+    const uint32_t M = 0u - diff;
+    unsigned c1, c2, c3;
+    const uint32_t s1 = __builtin_addc(b1 ^ M, ((uint32_t) ma << 30) | diff, 0u, &c1);
+    const uint32_t s2 = __builtin_addc((uint32_t) bh ^ M, (uint32_t) ah, c1, &c2);
+    const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32) ^ M, (uint32_t) (ah >> 32), c2, &c3);
+    (void) c3;
+    // normalise: bit 127 is clear, so a valid lz is 1..31; ~0 (top word 0,
+    // or ~0 for a negative S) saturates E to 0, flagged below
+    const uint32_t lz = ffbh_signed(s3);
+    uint64_t hi = ((uint64_t) s3 << 32) | s2;
+    hi = (hi << (lz & 63)) | ((s1 >> 1) >> ((31u - lz) & 31));
+    const uint32_t lo1 = s1 << (lz & 31);  // the low word of lo stays 0
+    const uint32_t E = sub_sat(EA + 2u, lz);
+    // RNE at bit 64, lo = lo1 * 2^32: up iff lo1 > 2^31, or lo1 == 2^31 and
+    // hi is odd, i.e. iff lo1 >= K = 2^31 + 1 - (hi & 1).  In borrows: the
+    // compare's borrow is !up, and hi - ~0 - borrow = hi + up word by word,
+    // each borrow out the complement of the carry (the last one, !wrap)
+    unsigned nup, nc, nwrap;
+    (void) __builtin_subc(lo1, (~(uint32_t) hi & 1u) | 0x80000000u, 0u, &nup);
+    const uint32_t h0 = __builtin_subc((uint32_t) hi, ~0u, nup, &nc);
+    const uint32_t hh = __builtin_subc((uint32_t) (hi >> 32), ~0u, nc, &nwrap);
+    *r = XU{((uint64_t) hh << 32) | h0, E, sign};
+    return !far && E - 1u < kEmax - 1u && nwrap;
+}
+
+// add_same_fast for two NORMAL operands of the SAME sign whose exponents
+// differ by at most 31 (false otherwise), by add_near's means: B's lowest
+// word is zero (one 32-bit left shift, one 64-bit right shift, no drop
+// mask), and the round's low word is zero (the borrow chain).  ~30 VALU per
+// add against add_same_fast's ~39.  false: gaps above 31, overflow, all ones
+// rounded up.
+OSGPU_HD inline bool add_same_near(XU a, XU b, XU *r)
+{
+    const bool swap = b.e > a.e;
+    const uint64_t ma = swap ? b.m : a.m;
+    const uint64_t mb = swap ? a.m : b.m;
+    const uint32_t EA = swap ? b.e : a.e;
+    const uint32_t d1 = absdiff15(a.e, b.e, 1u);  // d + 1
+    unsigned far;  // d1 > 32: a gap above 31
+    const uint32_t b1 = (uint32_t) mb << (__builtin_subc(32u, d1, 0u, &far) & 31);
+    const uint64_t bh = mb >> (d1 & 63);
+    const uint64_t ah = ma >> 1;
+    unsigned c1, c2, c3;
+    const uint32_t s1 = __builtin_addc(b1, (uint32_t) ma << 31, 0u, &c1);
+    const uint32_t s2 = __builtin_addc((uint32_t) bh, (uint32_t) ah, c1, &c2);
+    const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32), (uint32_t) (ah >> 32), c2, &c3);
+    (void) c3;
+    uint64_t hi = ((uint64_t) s3 << 32) | s2;
+    const uint32_t top = s3 >> 31, t = top ^ 1u;
+    hi = (hi << t) | ((s1 >> 31) & t);
+    const uint32_t lo1 = s1 << t;
+    const uint32_t E = EA + top;  // EA + 1 - lz, lz = t
+    unsigned nup, nc, nwrap;
+    (void) __builtin_subc(lo1, (~(uint32_t) hi & 1u) | 0x80000000u, 0u, &nup);
+    const uint32_t h0 = __builtin_subc((uint32_t) hi, ~0u, nup, &nc);
+    const uint32_t hh = __builtin_subc((uint32_t) (hi >> 32), ~0u, nc, &nwrap);
+    *r = XU{((uint64_t) hh << 32) | h0, E, a.s};
+    return !far && nwrap && E < kEmax;
 }
 
 // true in every lane of the wave (device), or for this element (host, where
@@ -401,14 +510,22 @@ OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
     return round_pack(s, E, P);
 }
 
-// The rounds of every member's fold (team_fold_sum_prod below).  ADD_ONLY:
-// every input of the element carries one sign, so every fold adds like
-// signs throughout (the exact sum of two values of sign s has sign s; a
-// NaN or infinity, whose sign may differ, is never normal, and a fold whose
-// value is not normal stays on the general op) -- the addition-only fast
-// add applies to every round.
-template <int OP, int P, bool ADD_ONLY>
-OSGPU_HD inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&acc)[P - 1],
+// The rounds of every member's fold (team_fold_sum_prod below), by the
+// fast op of MODE, add_general / mul_general for the folds and lanes it
+// does not cover:
+//  * F_FULL: add_fast / mul_fast;
+//  * F_NEAR: add_near (exponent gaps up to 30);
+//  * F_SAME, F_SAME_NEAR: every input of the element carries one sign, so
+//    every fold adds like signs throughout (the exact sum of two values of
+//    sign s has sign s; a NaN or infinity, whose sign may differ, is never
+//    normal, and a fold whose value is not normal stays on the general op)
+//    -- add_same_fast, or add_same_near (gaps up to 31).
+enum FoldMode { F_FULL, F_NEAR, F_SAME, F_SAME_NEAR };
+
+// Folds F0..F1-1 through every round.
+
+template <int OP, int P, int MODE, int F0, int F1>
+OSGPU_HD __attribute__((always_inline)) inline void fold_group(const XU (&u)[P], const bool (&nrm)[P], XU (&acc)[P - 1],
                                  bool (&slow)[P - 1])
 {
     constexpr int NF = P - 1;
@@ -418,18 +535,20 @@ OSGPU_HD inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&ac
         bool ok[NF];
         bool all = true;
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
+        for (int f = F0; f < F1; f++) {
             const int q = f == 0 ? 0 : f + 1;
             const int j = t < q ? t : t + 1;  // q's t-th operand
             const bool fast = OP == 1 ? mul_fast(acc[f], u[j], &res[f])
-                              : ADD_ONLY ? add_same_fast(acc[f], u[j], &res[f])
-                                         : add_fast(acc[f], u[j], &res[f]);
+                              : MODE == F_SAME ? add_same_fast(acc[f], u[j], &res[f])
+                              : MODE == F_SAME_NEAR ? add_same_near(acc[f], u[j], &res[f])
+                              : MODE == F_NEAR ? add_near(acc[f], u[j], &res[f])
+                                               : add_fast(acc[f], u[j], &res[f]);
             ok[f] = fast && !slow[f] && nrm[j];
             all = all && ok[f];
         }
         if (!all) {
 #pragma unroll
-            for (int f = 0; f < NF; f++) {
+            for (int f = F0; f < F1; f++) {
                 if (!ok[f]) {
                     const int q = f == 0 ? 0 : f + 1;
                     const int j = t < q ? t : t + 1;
@@ -440,8 +559,23 @@ OSGPU_HD inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&ac
             }
         }
 #pragma unroll
-        for (int f = 0; f < NF; f++) acc[f] = res[f];
+        for (int f = F0; f < F1; f++) acc[f] = res[f];
     }
+}
+
+// The P-1 folds in two groups, each through all its rounds before the next:
+// 3-4 independent chains per round are ILP enough beside the other waves of
+// the SIMD, and half the adds in flight keep the 8-member sum within 4 waves'
+// 128 VGPRs (10 spilled against 57 with all 7 folds per round; 1.18x the
+// random-sign 8-member sum, 1.03-1.05x the same-sign ones, in one process on
+// the same arrays: profiles/r06_ld_variants.jsonl).
+template <int OP, int P, int MODE>
+OSGPU_HD __attribute__((always_inline)) inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&acc)[P - 1],
+                                 bool (&slow)[P - 1])
+{
+    constexpr int H = P / 2;
+    fold_group<OP, P, MODE, 0, H>(u, nrm, acc, slow);
+    fold_group<OP, P, MODE, H, P - 1>(u, nrm, acc, slow);
 }
 
 // Every member's fold of a P-PE sum (OP 0) or prod (OP 1) of one element,
@@ -451,27 +585,35 @@ OSGPU_HD inline void fold_rounds(const XU (&u)[P], const bool (&nrm)[P], XU (&ac
 // member 1's fold x1 op x0 op x2 ... equals member 0's: P-1 folds, not P.
 //
 // The folds advance in rounds: round t applies every fold's t-th operand
-// with the straight-line fast op, so the P-1 independent chains interleave
-// in one instruction stream (ILP for a VALU-bound kernel); only when some
+// with the straight-line fast op, so independent chains interleave in one
+// instruction stream (ILP for a VALU-bound kernel; fold_rounds); only when some
 // lane of the wave has an operand or result outside the fast op's range
-// does the round take the general op, for those folds and lanes.  A fold
+// does the round take the slower op, for those folds and lanes.  A fold
 // whose running value leaves the normal range stays on the general op
-// (`slow`) until it is normal again.  A sum whose inputs all carry one sign
-// in every lane of the wave (sums of same-sign data) runs every round on
-// the addition-only fast add (add_same_fast; chosen once per element, a
-// wave-uniform branch).
+// (`slow`) until it is normal again.  The fast add is chosen once per
+// element, wave-uniform branches: a sum whose inputs' biased exponents lie
+// within kNearSpread of each other in every lane of the wave takes the
+// near-exponent adds (a running sum stays within a few binades of its inputs
+// unless it cancels by 6+ bits, and a fold that then meets a wider gap takes
+// the general add for that round), the same-sign form where every input of
+// every lane carries one sign; other sums take add_fast / add_same_fast.
+constexpr uint32_t kNearSpread = 24;
+
 template <int OP, int P>
-OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
+OSGPU_HD __attribute__((always_inline)) inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
 {
     constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
     XU u[P];
     bool nrm[P];
     bool same = OP == 0;
+    uint32_t emax = 0, emin = kEmax;
 #pragma unroll
     for (int p = 0; p < P; p++) {
         u[p] = unpack_u(x[p]);
         nrm[p] = normal_u(u[p]);
         same = same && u[p].s == u[0].s;
+        emax = u[p].e > emax ? u[p].e : emax;
+        emin = u[p].e < emin ? u[p].e : emin;
     }
     XU acc[NF];
     bool slow[NF];
@@ -481,10 +623,17 @@ OSGPU_HD inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
         acc[f] = u[q];
         slow[f] = !nrm[q];
     }
-    if (OP == 0 && wave_all(same))
-        fold_rounds<OP, P, true>(u, nrm, acc, slow);
-    else
-        fold_rounds<OP, P, false>(u, nrm, acc, slow);
+    const bool near = OP == 0 && wave_all(emax - emin <= kNearSpread);
+    if (OP == 0 && wave_all(same)) {
+        if (near)
+            fold_rounds<OP, P, F_SAME_NEAR>(u, nrm, acc, slow);
+        else
+            fold_rounds<OP, P, F_SAME>(u, nrm, acc, slow);
+    } else if (near) {
+        fold_rounds<OP, P, F_NEAR>(u, nrm, acc, slow);
+    } else {
+        fold_rounds<OP, P, F_FULL>(u, nrm, acc, slow);
+    }
 #pragma unroll
     for (int f = 0; f < NF; f++) out[f == 0 ? 0 : f + 1] = pack_u(acc[f]);
     out[1] = out[0];

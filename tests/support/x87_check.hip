@@ -24,6 +24,17 @@ extern "C" int x87check_op(int op, const void *a, const void *b, void *out, size
         X80 x = ld(A + 16 * i), y = ld(B + 16 * i), r;
         switch (op) {
         case 0: r = add(x, y); break;
+        case 10: {  // the near-exponent rounds' add: add_near where it applies, else add
+            XU ua = unpack_u(x), ub = unpack_u(y), ur;
+            r = normal_u(ua) && normal_u(ub) && add_near(ua, ub, &ur) ? pack_u(ur) : add(x, y);
+            break;
+        }
+        case 11: {  // the same-sign near rounds' add, where the signs agree
+            XU ua = unpack_u(x), ub = unpack_u(y), ur;
+            r = ua.s == ub.s && normal_u(ua) && normal_u(ub) && add_same_near(ua, ub, &ur)
+                    ? pack_u(ur) : add(x, y);
+            break;
+        }
         case 1: r = mul(x, y); break;
         case 5: r = less(y, x) ? x : y; break;
         case 6: r = less(x, y) ? x : y; break;

@@ -8,9 +8,10 @@ notes read with llvm-readelf, parsed by tools/isa/reg_table.py.
 * every kernel keeps at least 2 waves per SIMD, every team kernel at least 3
   (complexf prod at 8 members ran at 1 wave with 276 VGPRs +
   20 AGPRs; now 134 VGPRs, 3 waves, the only team kernel above 128);
-* no scratch, except the x87 long double 8-member sum/prod team kernel
-  (64 B per lane for 2 spilled VGPRs at 128 VGPRs, 4 waves per SIMD: the
-  trade its round-3 tuning made).
+* no scratch, except the x87 long double 7- and 8-member sum team kernels
+  (at most 64 B per lane -- 16 / 48 B for 2 / 10 spilled VGPRs at 128
+  VGPRs, 4 waves per SIMD: the trade of x87.hpp fold_rounds, whose two
+  groups of folds took the 8-member sum from 57 spilled VGPRs to 10).
 
 Skipped when the objects or the LLVM tools are absent (e.g. on the GPU box,
 where only the linked library travels).
@@ -75,7 +76,8 @@ def test_no_scratch_except_the_x87_team_fold(kernels):
     bad = []
     for o, rows in kernels.items():
         for r in rows:
-            allowed = 64 if "x87::ld_team_kernel<" in r["kernel"] and ", 8, " in r["kernel"] else 0
+            allowed = 64 if "x87::ld_team_kernel<0" in r["kernel"] and (
+                ", 7, " in r["kernel"] or ", 8, " in r["kernel"]) else 0
             if r["scratch"] > allowed:
                 bad.append((o, r["kernel"][:100], r["scratch"], r["vgpr_spill"]))
     assert not bad, json.dumps(bad[:10])

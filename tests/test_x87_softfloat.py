@@ -15,7 +15,9 @@ import oracle as O
 from support import team as T
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-OPS = ((0, "sum"), (1, "prod"), (5, "max"), (6, "min"))
+OPS = ((0, "sum"), (1, "prod"), (5, "max"), (6, "min"),
+       (10, "sum"),   # 10: add_near where it applies (x87_check.hip), else add
+       (11, "sum"))   # 11: add_same_near where the signs agree, else add
 
 
 @pytest.fixture(scope="module")
@@ -92,7 +94,7 @@ def test_cancellation(x87):
 def _pairs(where, n=60_000):
     r = O.splitmix64(77, 4 * n).reshape(4, n)
     base_e = {"unit": 16383, "underflow": 3, "overflow": 0x7FFE - 1}[where]
-    diffs = np.array([0, 1, 2, 3, 62, 63, 64, 65, 66, 67, 70, 120, 200], np.int64)
+    diffs = np.array([0, 1, 2, 3, 29, 30, 31, 32, 62, 63, 64, 65, 66, 67, 70, 120, 200], np.int64)
     d = diffs[r[0] % np.uint64(diffs.size)]
     ea = np.full(n, base_e, np.int64) + (r[1] % np.uint64(3)).astype(np.int64) - 1
     eb = np.clip(ea - d, 1, 0x7FFE)
@@ -229,6 +231,84 @@ def test_team_fold_rounds(x87, op, P):
     sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in srcs])
     dp = (ctypes.c_void_p * P)(*[g.ctypes.data for g in got])
     assert x87.x87check_team(0 if op == "sum" else 1, P, sp, dp, n) == 0
+    for q in range(P):
+        w = O.value_bytes(want[q]).reshape(-1, 10)
+        g = O.value_bytes(got[q]).reshape(-1, 10)
+        bad = np.nonzero((w != g).any(1))[0]
+        assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"
+
+
+def test_tie_of_exponent_and_top_word(x87):
+    """Operands with the same exponent and the same top 32 significand bits
+    (the magnitude order's tie, x87.hpp add_fast's flag and add_near's
+    negative-sum case): low words random, equal or one apart, both signs
+    pairings, both operand orders."""
+    n = 100_000
+    r = O.splitmix64(61, 4 * n).reshape(4, n)
+    hi = (r[0] | np.uint64(1 << 63)) & np.uint64(0xFFFFFFFF00000000)
+    lo_a = r[1] & np.uint64(0xFFFFFFFF)
+    kind = r[2] % np.uint64(3)
+    lo_b = np.where(kind == 0, r[3] & np.uint64(0xFFFFFFFF),
+                    np.where(kind == 1, lo_a, (lo_a + np.uint64(1)) & np.uint64(0xFFFFFFFF)))
+    e = np.full(n, 16383, np.uint64) + (r[2] >> np.uint64(8)) % np.uint64(40) - np.uint64(20)
+    sa = (r[3] >> np.uint64(40)) & np.uint64(1)
+    sb = np.where((r[3] >> np.uint64(41)) & np.uint64(3) == 0, sa, sa ^ np.uint64(1))
+
+    def pack(m, sg):
+        arr = np.zeros((n, 16), np.uint8)
+        arr[:, :8] = m.astype(np.uint64).view(np.uint8).reshape(n, 8)
+        arr[:, 8:10] = (e | (sg << np.uint64(15))).astype(np.uint16).view(np.uint8).reshape(n, 2)
+        return arr.reshape(-1).view(np.longdouble)
+    a, b = pack(hi | lo_a, sa), pack(hi | lo_b, sb)
+    check(x87, a, b, use_ref=O.ref_lib() is not None)
+    check(x87, b, a, use_ref=O.ref_lib() is not None)
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_team_fold_near(x87, P):
+    """Sums whose inputs' exponents lie within x87.hpp kNearSpread of each
+    other take the near-exponent rounds (add_near, falling back to add_fast
+    and add_general per fold): random signs, exponents 2^-3..2^3 (the bench's
+    data), near-cancellations of the first two operands (the running sum
+    drops 20-60 binades below the next operand: gaps above 30 in later
+    rounds), exact cancellations, top-word ties, and some elements whose
+    inputs spread wider (the general rounds) -- against the reference's
+    per-PE fold order."""
+    n = 40_000
+    srcs = []
+    for p in range(P):
+        r = O.splitmix64(1200 + p, 2 * n).reshape(2, n)
+        m = r[0] | np.uint64(1 << 63)
+        e = np.full(n, 16383, np.uint64) + r[1] % np.uint64(7) - np.uint64(3)
+        wide = (r[1] >> np.uint64(20)) % np.uint64(11) == np.uint64(0)
+        e = np.where(wide, e + (r[1] >> np.uint64(24)) % np.uint64(60), e)
+        s = (r[1] >> np.uint64(40)) & np.uint64(1)
+        arr = np.zeros((n, 16), np.uint8)
+        arr[:, :8] = m.view(np.uint8).reshape(n, 8)
+        arr[:, 8:10] = (e | (s << np.uint64(15))).astype(np.uint16).view(np.uint8).reshape(n, 2)
+        srcs.append(arr.reshape(-1).view(np.longdouble).copy())
+    # element k % 5 == 1: x1 = -x0 * (1 + 2^-j * u), j in 20..60; k % 5 == 2:
+    # x1 = -x0 exactly; k % 5 == 3: x1 = x0's exponent and top word, opposite sign
+    x0 = O.value_bytes(srcs[0]).reshape(-1, 10).copy()
+    x1 = O.value_bytes(srcs[1]).reshape(-1, 10).copy()
+    k = np.arange(n)
+    j = 20 + (k * 7) % 41
+    u = O.splitmix64(1300, n).astype(np.longdouble) / np.longdouble(2.0 ** 64)
+    near = -srcs[0] * (np.longdouble(1) + np.ldexp(np.longdouble(1), -j) * u)
+    nb = O.value_bytes(near).reshape(-1, 10)
+    x1[k % 5 == 1] = nb[k % 5 == 1]
+    neg = x0.copy()
+    neg[:, 9] ^= 0x80
+    x1[k % 5 == 2] = neg[k % 5 == 2]
+    tie = neg.copy()
+    tie[:, :4] = x1[:, :4]
+    x1[k % 5 == 3] = tie[k % 5 == 3]
+    srcs[1] = np.ascontiguousarray(O.from_value_bytes("longdouble", x1.reshape(-1)))
+    want = O.to_all("longdouble", "sum", srcs)
+    got = [np.zeros_like(srcs[0]) for _ in range(P)]
+    sp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in srcs])
+    dp = (ctypes.c_void_p * P)(*[g.ctypes.data for g in got])
+    assert x87.x87check_team(0, P, sp, dp, n) == 0
     for q in range(P):
         w = O.value_bytes(want[q]).reshape(-1, 10)
         g = O.value_bytes(got[q]).reshape(-1, 10)

@@ -7,7 +7,7 @@ log=$1; to=$2; cmd=$3
 for i in $(seq 1 ${RETRIES:-12}); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
-  if grep -q "no free box\|status=transient\|backing off\|taken away by the GPU service\|stopped responding while being prepared" "$log" && ! grep -q "all steps done" "$log"; then
+  if grep -q "no free box\|status=transient\|backing off\|taken away by the GPU service\|stopped responding while being prepared\|GPU slot(s) on this pod are busy" "$log" && ! grep -q "all steps done" "$log"; then
     echo "attempt $i: no box ($rc), retrying" >> "$log.attempts"
     sleep ${RETRY_SLEEP:-120}
     continue

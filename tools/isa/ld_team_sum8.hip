@@ -7,7 +7,7 @@ struct LdTeam { const unsigned char *src[8]; unsigned char *dst[8]; };
 __device__ __forceinline__ X80 unpack(u64x2 v) { return X80{v.x, (uint32_t) (v.y & 0xffffu)}; }
 __device__ __forceinline__ u64x2 pack(X80 x) { u64x2 v; v.x = x.m; v.y = (unsigned long long) (x.se & 0xffffu); return v; }
 template <int OP, int P>
-__global__ __launch_bounds__(256) void ldk(LdTeam a, size_t n)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ldk(LdTeam a, size_t n)
 {
     const size_t stride = (size_t) gridDim.x * blockDim.x;
     for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {

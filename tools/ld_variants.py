@@ -26,7 +26,7 @@ CSRC = os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc")
 VAR = os.path.join(ROOT, "tools", "variants")
 FL = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
       "-fno-fast-math"]
-OTHERS = ["combine.o", "team.o", "fused.o", "verify.o", "copy.o", "runtime.o", "heap.o",
+OTHERS = ["combine.o", "team.o", "fused.o", "verify.o", "copy.o", "host_fold.o", "runtime.o", "heap.o",
           "shmem_reduce.o", "shmem_collect.o"]
 
 
@@ -41,7 +41,10 @@ def variants():
 def build():
     subprocess.run(["make", "-s", "-j8"], cwd=CSRC, check=True)
     procs = []
-    for name, src in variants().items():
+    # LDV_BUILD=a,b: build only those (the others' libraries stay as they are)
+    only = set(filter(None, os.environ.get("LDV_BUILD", "").split(",")))
+    todo = {k: v for k, v in variants().items() if not only or k in only}
+    for name, src in todo.items():
         d = os.path.join(VAR, "ld_" + name)
         s = os.path.join(d, "src")
         os.makedirs(s, exist_ok=True)
@@ -57,7 +60,7 @@ def build():
         procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + FL + ["-c", os.path.join(s, "longdouble.hip"),
                                                                       "-o", os.path.join(d, "longdouble.o")]))
     assert all(p.wait() == 0 for p in procs)
-    for name in variants():
+    for name in todo:
         d = os.path.join(VAR, "ld_" + name)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                         os.path.join(d, "libosgpu_reduce.so"), os.path.join(d, "longdouble.o")] +
