@@ -105,11 +105,14 @@ OSGPU_HD __attribute__((noinline)) inline X80 add_general(X80 a, X80 b);
 struct XU {
     uint64_t m;
     uint32_t e;  // biased exponent, 0..0x7fff
-    uint32_t s;  // sign, 0 or 1
+    uint32_t s;  // sign as a mask: 0 (+) or ~0 (-)
 };
 
-OSGPU_HD inline XU unpack_u(X80 x) { return XU{x.m, x.se & kEmax, (x.se >> 15) & 1}; }
-OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s << 15) | x.e}; }
+OSGPU_HD inline XU unpack_u(X80 x)
+{
+    return XU{x.m, x.se & kEmax, (uint32_t) ((int32_t) (x.se << 16) >> 31)};
+}
+OSGPU_HD inline X80 pack_u(XU x) { return X80{x.m, (x.s & 0x8000u) | x.e}; }
 
 OSGPU_HD inline bool normal_u(XU x) { return x.e - 1u < kEmax - 1u && (x.m >> 63); }
 
@@ -193,8 +196,8 @@ OSGPU_HD inline bool add_fast(XU a, XU b, XU *r)
     const uint64_t ah = ma >> 1, bh = mb >> ((d + 1) & 63), bl = mb << ((63 - d) & 63);
     // S = A + B, or A - B as A + ~B + 1, in 32-bit words with explicit
     // carries (A's lowest word is 0; the + 1 rides in as the first carry)
-    const uint32_t diff = a.s ^ b.s;
-    const uint32_t M = 0u - diff;
+    const uint32_t M = a.s ^ b.s;  // ~0 to subtract
+    const uint32_t diff = M & 1u;
     unsigned c0, c1, c2, c3;
     const uint32_t s0 = __builtin_addc((uint32_t) bl ^ M, 0u, diff, &c0);
     const uint32_t s1 = __builtin_addc((uint32_t) (bl >> 32) ^ M, (uint32_t) ma << 31, c0, &c1);
@@ -280,6 +283,16 @@ OSGPU_HD inline uint32_t ffbh_signed(uint32_t x)
 #endif
 }
 
+// low 32 bits of (hi:lo) >> (n & 31) (one v_alignbit_b32)
+OSGPU_HD inline uint32_t funnel_r(uint32_t hi, uint32_t lo, uint32_t n)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+    return (uint32_t) ((((uint64_t) hi << 32) | lo) >> (n & 31));
+#endif
+}
+
 // add_fast for two NORMAL operands whose exponents differ by at most 30
 // (the caller checks nothing; false otherwise): the same exact-then-round
 // sum, two bits lower -- A = ma * 2^62, B = mb * 2^(62-d) -- which buys:
@@ -295,9 +308,12 @@ OSGPU_HD inline uint32_t ffbh_signed(uint32_t x)
 //    leading-bit count (~0 for 0 and for ~0) flags it through the exponent
 //    range test with the 32-bit cancellations: no tie compare;
 //  * the round's low word is zero: one 32-bit carry test.
-// 41 VALU per add against add_fast's 51, ~1070 issue cycles per round of 7
-// adds against ~1290 (tools/isa/count_ld_valu.sh).  false: gaps above 30, cancellations of 32 bits or more, negative S,
-// results outside the normal range, all ones rounded up.
+//  * bit 127 clear also makes every valid leading-zero count 1..31, so the
+//    normalising left shift is two funnel shifts right by 32 - lz.
+// Precondition (the caller's): 30 <= max(a.e, b.e) <= kEmax - 2, so the
+// result's exponent needs no range test.  ~38 VALU per add against
+// add_fast's 51 (tools/isa/count_ld_valu.sh).  false: gaps above 30,
+// cancellations of 32 bits or more, negative S, all ones rounded up.
 OSGPU_HD inline bool add_near(XU a, XU b, XU *r)
 {
     const uint64_t ka = ((uint64_t) a.e << 32) | (uint32_t) (a.m >> 32);
@@ -314,20 +330,25 @@ OSGPU_HD inline bool add_near(XU a, XU b, XU *r)
     const uint32_t b1 = (uint32_t) mb << (__builtin_subc(32u, d2, 0u, &far) & 31);
     const uint64_t bh = mb >> (d2 & 63);
     const uint64_t ah = ma >> 2;
-    const uint32_t diff = a.s ^ b.s;
-    const uint32_t M = 0u - diff;
+    const uint32_t M = a.s ^ b.s;  // ~0 to subtract
+    const uint32_t diff = M & 1u;
     unsigned c1, c2, c3;
     const uint32_t s1 = __builtin_addc(b1 ^ M, ((uint32_t) ma << 30) | diff, 0u, &c1);
     const uint32_t s2 = __builtin_addc((uint32_t) bh ^ M, (uint32_t) ah, c1, &c2);
     const uint32_t s3 = __builtin_addc((uint32_t) (bh >> 32) ^ M, (uint32_t) (ah >> 32), c2, &c3);
     (void) c3;
-    // normalise: bit 127 is clear, so a valid lz is 1..31; ~0 (top word 0,
-    // or ~0 for a negative S) saturates E to 0, flagged below
+    // normalise: bit 127 is clear, so a valid lz is 1..31 and the left
+    // shift of (s3, s2, s1) is two funnel shifts right by 32 - lz; ~0 (top
+    // word 0, or ~0 for a negative S) borrows in E, flagged below
     const uint32_t lz = ffbh_signed(s3);
-    uint64_t hi = ((uint64_t) s3 << 32) | s2;
-    hi = (hi << (lz & 63)) | ((s1 >> 1) >> ((31u - lz) & 31));
+    const uint32_t rs = (0u - lz) & 31;  // 32 - lz
+    const uint32_t hh0 = funnel_r(s3, s2, rs), hl0 = funnel_r(s2, s1, rs);
+    const uint64_t hi = ((uint64_t) hh0 << 32) | hl0;
     const uint32_t lo1 = s1 << (lz & 31);  // the low word of lo stays 0
-    const uint32_t E = sub_sat(EA + 2u, lz);
+    // E = EA + 2 - lz lies in [EA - 29, EA + 1], inside [1, kEmax) under the
+    // precondition 30 <= EA <= kEmax - 2: only lz = ~0 borrows
+    unsigned low;
+    const uint32_t E = __builtin_subc(EA + 2u, lz, 0u, &low);
     // RNE at bit 64, lo = lo1 * 2^32: up iff lo1 > 2^31, or lo1 == 2^31 and
     // hi is odd, i.e. iff lo1 >= K = 2^31 + 1 - (hi & 1).  In borrows: the
     // compare's borrow is !up, and hi - ~0 - borrow = hi + up word by word,
@@ -337,15 +358,16 @@ OSGPU_HD inline bool add_near(XU a, XU b, XU *r)
     const uint32_t h0 = __builtin_subc((uint32_t) hi, ~0u, nup, &nc);
     const uint32_t hh = __builtin_subc((uint32_t) (hi >> 32), ~0u, nc, &nwrap);
     *r = XU{((uint64_t) hh << 32) | h0, E, sign};
-    return !far && E - 1u < kEmax - 1u && nwrap;
+    return !far && !low && nwrap;
 }
 
 // add_same_fast for two NORMAL operands of the SAME sign whose exponents
 // differ by at most 31 (false otherwise), by add_near's means: B's lowest
 // word is zero (one 32-bit left shift, one 64-bit right shift, no drop
 // mask), and the round's low word is zero (the borrow chain).  ~30 VALU per
-// add against add_same_fast's ~39.  false: gaps above 31, overflow, all ones
-// rounded up.
+// add against add_same_fast's ~39.  Precondition: max(a.e, b.e) <= kEmax - 2
+// (E <= EA + 1 needs no range test).  false: gaps above 31, all ones rounded
+// up.
 OSGPU_HD inline bool add_same_near(XU a, XU b, XU *r)
 {
     const bool swap = b.e > a.e;
@@ -372,7 +394,7 @@ OSGPU_HD inline bool add_same_near(XU a, XU b, XU *r)
     const uint32_t h0 = __builtin_subc((uint32_t) hi, ~0u, nup, &nc);
     const uint32_t hh = __builtin_subc((uint32_t) (hi >> 32), ~0u, nc, &nwrap);
     *r = XU{((uint64_t) hh << 32) | h0, E, a.s};
-    return !far && nwrap && E < kEmax;
+    return !far && nwrap;
 }
 
 // true in every lane of the wave (device), or for this element (host, where
@@ -529,6 +551,12 @@ OSGPU_HD __attribute__((always_inline)) inline void fold_group(const XU (&u)[P],
                                  bool (&slow)[P - 1])
 {
     constexpr int NF = P - 1;
+    // the near modes' gate (team_fold_sum_prod) makes every input normal
+    // and every add meet the near adds' precondition; a running sum that
+    // left the normal range (a cancellation to zero or below 2^-16351) has
+    // exponent 0, more than 30 below the input's: the near add flags it
+    // itself, so these rounds need no `slow` / `nrm` terms
+    constexpr bool NEAR = MODE == F_NEAR || MODE == F_SAME_NEAR;
 #pragma unroll
     for (int t = 0; t < P - 1; t++) {
         XU res[NF];
@@ -543,7 +571,7 @@ OSGPU_HD __attribute__((always_inline)) inline void fold_group(const XU (&u)[P],
                               : MODE == F_SAME_NEAR ? add_same_near(acc[f], u[j], &res[f])
                               : MODE == F_NEAR ? add_near(acc[f], u[j], &res[f])
                                                : add_fast(acc[f], u[j], &res[f]);
-            ok[f] = fast && !slow[f] && nrm[j];
+            ok[f] = NEAR ? fast : fast && !slow[f] && nrm[j];
             all = all && ok[f];
         }
         if (!all) {
@@ -554,7 +582,7 @@ OSGPU_HD __attribute__((always_inline)) inline void fold_group(const XU (&u)[P],
                     const int j = t < q ? t : t + 1;
                     res[f] = unpack_u(OP == 0 ? add_general(pack_u(acc[f]), pack_u(u[j]))
                                               : mul_general(pack_u(acc[f]), pack_u(u[j])));
-                    slow[f] = !normal_u(res[f]);
+                    if (!NEAR) slow[f] = !normal_u(res[f]);
                 }
             }
         }
@@ -598,6 +626,11 @@ OSGPU_HD __attribute__((always_inline)) inline void fold_rounds(const XU (&u)[P]
 // the general add for that round), the same-sign form where every input of
 // every lane carries one sign; other sums take add_fast / add_same_fast.
 constexpr uint32_t kNearSpread = 24;
+// and whose inputs are all normal with exponents in [kNearEmin, kNearEmax]:
+// every add of the fold then meets the near adds' precondition (EA >= the
+// input's exponent >= 32; a running sum grows by at most one binade per
+// round, 7 rounds)
+constexpr uint32_t kNearEmin = 32, kNearEmax = kEmax - 16;
 
 template <int OP, int P>
 OSGPU_HD __attribute__((always_inline)) inline void team_fold_sum_prod(const X80 (&x)[P], X80 (&out)[P])
@@ -605,12 +638,13 @@ OSGPU_HD __attribute__((always_inline)) inline void team_fold_sum_prod(const X80
     constexpr int NF = P - 1;  // folds of members 0, 2, 3, ..., P-1
     XU u[P];
     bool nrm[P];
-    bool same = OP == 0;
+    bool same = OP == 0, allnrm = true;
     uint32_t emax = 0, emin = kEmax;
 #pragma unroll
     for (int p = 0; p < P; p++) {
         u[p] = unpack_u(x[p]);
         nrm[p] = normal_u(u[p]);
+        allnrm = allnrm && nrm[p];
         same = same && u[p].s == u[0].s;
         emax = u[p].e > emax ? u[p].e : emax;
         emin = u[p].e < emin ? u[p].e : emin;
@@ -623,7 +657,8 @@ OSGPU_HD __attribute__((always_inline)) inline void team_fold_sum_prod(const X80
         acc[f] = u[q];
         slow[f] = !nrm[q];
     }
-    const bool near = OP == 0 && wave_all(emax - emin <= kNearSpread);
+    const bool near = OP == 0 && wave_all(allnrm && emax - emin <= kNearSpread &&
+                                          emin >= kNearEmin && emax <= kNearEmax);
     if (OP == 0 && wave_all(same)) {
         if (near)
             fold_rounds<OP, P, F_SAME_NEAR>(u, nrm, acc, slow);

@@ -26,12 +26,15 @@ extern "C" int x87check_op(int op, const void *a, const void *b, void *out, size
         case 0: r = add(x, y); break;
         case 10: {  // the near-exponent rounds' add: add_near where it applies, else add
             XU ua = unpack_u(x), ub = unpack_u(y), ur;
-            r = normal_u(ua) && normal_u(ub) && add_near(ua, ub, &ur) ? pack_u(ur) : add(x, y);
+            const uint32_t EA = ua.e > ub.e ? ua.e : ub.e;  // add_near's precondition
+            r = normal_u(ua) && normal_u(ub) && EA >= 30 && EA <= kEmax - 2 && add_near(ua, ub, &ur)
+                    ? pack_u(ur) : add(x, y);
             break;
         }
         case 11: {  // the same-sign near rounds' add, where the signs agree
             XU ua = unpack_u(x), ub = unpack_u(y), ur;
-            r = ua.s == ub.s && normal_u(ua) && normal_u(ub) && add_same_near(ua, ub, &ur)
+            r = ua.s == ub.s && normal_u(ua) && normal_u(ub) && ua.e <= kEmax - 2 &&
+                        ub.e <= kEmax - 2 && add_same_near(ua, ub, &ur)
                     ? pack_u(ur) : add(x, y);
             break;
         }
