@@ -21,7 +21,7 @@ import pytest
 
 import oracle as O
 import osgpu
-from test_x87_softfloat import _deep_cancel_pairs, _pairs, raw_random
+from test_x87_softfloat import _deep_cancel_pairs, _pairs, near_bounds_srcs, raw_random
 
 pytestmark = pytest.mark.gpu
 
@@ -132,3 +132,28 @@ def test_team_folds_rate_data(torch_cuda, P, signs, op):
     for q in range(P):
         got = outs[q].cpu().numpy().reshape(-1, 16)[:, :10].reshape(-1)
         assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (op, P, signs, q)
+
+
+@pytest.mark.parametrize("P", [3, 8])
+@pytest.mark.parametrize("signs", ["random", "one"])
+def test_team_folds_near_exponent_bounds(torch_cuda, P, signs):
+    """The device team kernel on near_bounds_srcs: waves whose inputs sit
+    below, at and above the near-exponent gate's edges (x87.hpp kNearEmin,
+    kNearEmax; the fold mode is chosen per wave), with near-cancellations
+    -- every member's result bit-exact against the oracle's per-PE fold."""
+    torch = torch_cuda
+    n = 40_000
+    srcs = near_bounds_srcs(P, signs, n)
+    want = O.to_all("longdouble", "sum", srcs)
+    ins = [_dev(torch, x) for x in srcs]
+    outs = [torch.zeros(n * 16, dtype=torch.uint8, device="cuda:0") for _ in range(P)]
+    S = (ctypes.c_void_p * P)(*[x.data_ptr() for x in ins])
+    D = (ctypes.c_void_p * P)(*[x.data_ptr() for x in outs])
+    torch.cuda.synchronize()
+    L = osgpu.load()
+    assert L.osgpu_team_combine(osgpu.TYPES.index("longdouble"), osgpu.OPS.index("sum"), P, D, S,
+                                n, None) == 0
+    torch.cuda.synchronize()
+    for q in range(P):
+        got = outs[q].cpu().numpy().reshape(-1, 16)[:, :10].reshape(-1)
+        assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (P, signs, q)

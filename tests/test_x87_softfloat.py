@@ -316,20 +316,18 @@ def test_team_fold_near(x87, P):
         assert bad.size == 0, f"member {q}: {bad.size} mismatches at {bad[:5]}"
 
 
-@pytest.mark.parametrize("P", [3, 8])
-@pytest.mark.parametrize("signs", ["random", "one"])
-def test_team_fold_near_exponent_bounds(x87, P, signs):
-    """The near-exponent rounds' gate (x87.hpp kNearEmin / kNearEmax: the
-    near adds skip the result's range test): every element's inputs drawn
-    from one exponent window of 25 binades -- just below the gate (1..25,
-    results on the denormal grid), at its lower edge (32..56), at its upper
-    edge (kEmax-40..kEmax-16) and above it (kEmax-25..kEmax-1, overflow) --
-    with random or one sign and near-cancellations of the first two
-    operands, against the reference's per-PE fold order."""
-    n = 40_000
+def near_bounds_srcs(P, signs, n=40_000):
+    """Inputs of test_team_fold_near_exponent_bounds (and its device twin in
+    test_gpu_x87.py): every run of 64 elements (one wave on the GPU, where
+    the fold mode is chosen per wave) draws its exponents from one window of
+    25 binades -- just below the near-exponent gate (1..25, results on the
+    denormal grid), at its lower edge (32..56), at its upper edge
+    (kEmax-40..kEmax-16) and above it (kEmax-25..kEmax-1, overflow) --
+    random or one sign, and for random signs near-cancellations
+    x1 = -x0 (1 + 2^-j u), j in 20..60, in every third element."""
     lows = np.array([1, 32, 0x7FFF - 40, 0x7FFF - 25], np.uint64)
-    r0 = O.splitmix64(1400, n)
-    base = lows[(r0 % np.uint64(4)).astype(np.int64)]
+    k = np.arange(n)
+    base = lows[(k // 64) % 4]
     srcs = []
     for p in range(P):
         r = O.splitmix64(1410 + p, 2 * n).reshape(2, n)
@@ -340,14 +338,25 @@ def test_team_fold_near_exponent_bounds(x87, P, signs):
         arr[:, :8] = m.view(np.uint8).reshape(n, 8)
         arr[:, 8:10] = (e | (s << np.uint64(15))).astype(np.uint16).view(np.uint8).reshape(n, 2)
         srcs.append(arr.reshape(-1).view(np.longdouble).copy())
-    if signs == "random":   # x1 = -x0 (1 + 2^-j u): the running sum drops 20..60 binades
-        k = np.arange(n)
+    if signs == "random":
         j = 20 + (k * 7) % 41
         u = O.splitmix64(1420, n).astype(np.longdouble) / np.longdouble(2.0 ** 64)
         near = O.value_bytes(-srcs[0] * (np.longdouble(1) + np.ldexp(np.longdouble(1), -j) * u)).reshape(-1, 10)
         x1 = O.value_bytes(srcs[1]).reshape(-1, 10).copy()
         x1[k % 3 == 1] = near[k % 3 == 1]
         srcs[1] = np.ascontiguousarray(O.from_value_bytes("longdouble", x1.reshape(-1)))
+    return srcs
+
+
+@pytest.mark.parametrize("P", [3, 8])
+@pytest.mark.parametrize("signs", ["random", "one"])
+def test_team_fold_near_exponent_bounds(x87, P, signs):
+    """The near-exponent rounds' gate (x87.hpp kNearEmin / kNearEmax: the
+    near adds skip the result's range test), on near_bounds_srcs' windows
+    below, at and above its edges, against the reference's per-PE fold
+    order."""
+    n = 40_000
+    srcs = near_bounds_srcs(P, signs, n)
     want = O.to_all("longdouble", "sum", srcs)
     got = [np.zeros_like(srcs[0]) for _ in range(P)]
     sp = (ctypes.c_void_p * P)(*[s_.ctypes.data for s_ in srcs])
