@@ -545,7 +545,6 @@ OSGPU_HD __attribute__((noinline)) inline X80 mul_general(X80 a, X80 b)
 enum FoldMode { F_FULL, F_NEAR, F_SAME, F_SAME_NEAR };
 
 // Folds F0..F1-1 through every round.
-
 template <int OP, int P, int MODE, int F0, int F1>
 OSGPU_HD __attribute__((always_inline)) inline void fold_group(const XU (&u)[P], const bool (&nrm)[P], XU (&acc)[P - 1],
                                  bool (&slow)[P - 1])
