@@ -9,9 +9,10 @@ notes read with llvm-readelf, parsed by tools/isa/reg_table.py.
   (complexf prod at 8 members ran at 1 wave with 276 VGPRs +
   20 AGPRs; now 134 VGPRs, 3 waves, the only team kernel above 128);
 * no scratch, except the x87 long double 7- and 8-member sum team kernels
-  (at most 64 B per lane -- 16 / 48 B for 2 / 10 spilled VGPRs at 128
-  VGPRs, 4 waves per SIMD: the trade of x87.hpp fold_rounds, whose two
-  groups of folds took the 8-member sum from 57 spilled VGPRs to 10).
+  (at most 64 B per lane; today 0 / 48 B, 9 spilled VGPRs at 8 members,
+  128 VGPRs, 4 waves per SIMD: the trade of x87.hpp fold_rounds, whose two
+  groups of folds took the 8-member sum from 57 spilled VGPRs to 10, the
+  sign mask and the near rounds' dropped terms to 9).
 
 Skipped when the objects or the LLVM tools are absent (e.g. on the GPU box,
 where only the linked library travels).

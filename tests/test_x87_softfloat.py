@@ -267,8 +267,8 @@ def test_tie_of_exponent_and_top_word(x87):
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
 def test_team_fold_near(x87, P):
     """Sums whose inputs' exponents lie within x87.hpp kNearSpread of each
-    other take the near-exponent rounds (add_near, falling back to add_fast
-    and add_general per fold): random signs, exponents 2^-3..2^3 (the bench's
+    other take the near-exponent rounds (add_near, falling back to
+    add_general per fold and lane): random signs, exponents 2^-3..2^3 (the bench's
     data), near-cancellations of the first two operands (the running sum
     drops 20-60 binades below the next operand: gaps above 30 in later
     rounds), exact cancellations, top-word ties, and some elements whose
