@@ -48,6 +48,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # member counts that kernel serves (OSGPU_TEAM_LDS_MIN_P, OSGPU_TEAM_LDS_MAX_P)
 TEAM_LDS_U = 1
 TEAM_LDS_P = (2, 4)
+# ... and the LDS form also at 8 members for real types other than FP
+# max/min (double sum among them), when no member is remote (TeamShape kLds)
+TEAM_LDS_EXTRA_P = (8,)
+
+
+def team_lds(P, remote=False):
+    """True where team.hip launches the LDS-staged kernel for double sum."""
+    if remote:
+        return 3 <= P <= 4
+    return TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1] or P in TEAM_LDS_EXTRA_P
+
 # the headline kernel: combine.hip's LDS-staged form at K = 2 inputs
 # (OSGPU_COMBINE_LDS_U2 = 2 vectors per lane), its rocprof / PMC key and label
 COMBINE_KERNEL = "combine_lds_kernel<double, 0, 2, 2>"
@@ -316,7 +327,7 @@ def live_traffic(n, members=(2, 4, 8), reps=5, timeout=120):
         return {"_error": "rocprofv3 not on PATH"}
     keys = {COMBINE_KERNEL: 24}
     for P in members:
-        keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1]
+        keys[(f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if team_lds(P)
               else f"team_vec_kernel<double, 0, {P}, true>")] = 16 * P
     tmp = tempfile.mkdtemp(prefix="osgpu_pmc_")
     dirs = {}
@@ -835,8 +846,9 @@ def team_kernel_rate(L, torch, n, reps, P=2, arrays=None, layout="alloc", canary
     can_after = canary() if canary is not None else None
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
-    # kernel (U = TEAM_LDS_U) at 2 to 4 members, the register kernel otherwise
-    lds = TEAM_LDS_P[0] <= P <= TEAM_LDS_P[1]
+    # kernel (U = TEAM_LDS_U) at 2 to 4 and at 8 members, the register kernel
+    # otherwise
+    lds = team_lds(P)
     kern = (f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if lds    # (PMC files' key)
             else f"team_vec_kernel<double, 0, {P}, true>")
     tr = load_traffic(kern, n)
@@ -1871,7 +1883,7 @@ def bench_multi(args):
             "bound": "xgmi", "achieved": per_dir, "peak": peak, "unit": "GB/s",
             "frac": per_dir / peak, "traffic": None,
             "kernel": (f"osgpu::team_lds_kernel<double, SUM, {world}>"
-                       if TEAM_LDS_P[0] <= world <= TEAM_LDS_P[1]
+                       if team_lds(world, remote=res["launch"].get("distinct_gpus", False))
                        else f"osgpu::team_vec_kernel<double, SUM, {world}>"),
             "note": (f"achieved = bytes each GPU receives over its {world - 1} peer link(s) per "
                      f"second: the shard reads from every peer plus every peer's writes of its "
