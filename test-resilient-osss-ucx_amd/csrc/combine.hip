@@ -20,6 +20,7 @@
 //    ragged n) are folded by the first lanes of workgroup 0, so one launch
 //    covers any n.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -231,6 +232,10 @@ __global__ __launch_bounds__(kBlock) void combine_scalar_kernel(T *out, Inputs<T
 
 // ------------------------------------------------------------------ launch
 
+static std::atomic<size_t> g_launch_threads{kMaxLaunchThreads};
+size_t max_launch_threads() { return g_launch_threads.load(std::memory_order_relaxed); }
+void set_max_launch_threads(size_t n) { g_launch_threads.store(n, std::memory_order_relaxed); }
+
 template <typename T, int OP, int K>
 static hipError_t launch_k(T *out, const T *const *srcs, size_t n, hipStream_t s)
 {
@@ -256,22 +261,37 @@ static hipError_t launch_k(T *out, const T *const *srcs, size_t n, hipStream_t s
     size_t nvec = (n - head) / W;
     size_t tail_start = head + nvec * W;
     int nedge = (int) (head + (n - tail_start));
+    // tiles of V vectors, one per workgroup of `threads`; at most
+    // max_launch_threads() per launch (combine.hpp): the first launch takes the
+    // edges, the others the next runs of tiles through shifted pointers
+    auto launch = [&](size_t V, unsigned threads, auto kernel) -> hipError_t {
+        size_t tiles = (nvec + V - 1) / V;
+        if (tiles == 0) tiles = 1;
+        const size_t lim = max_launch_threads() / threads;
+        const size_t per_launch = lim ? lim : 1;
+        for (size_t t0 = 0; t0 < tiles; t0 += per_launch) {
+            const size_t nt = tiles - t0 < per_launch ? tiles - t0 : per_launch;
+            const size_t nv = nvec - t0 * V < nt * V ? nvec - t0 * V : nt * V;
+            if (t0 == 0) {
+                hipLaunchKernelGGL(kernel, dim3((unsigned) nt), dim3(threads), 0, s, out, in, nv,
+                                   head, tail_start, nedge);
+            } else {
+                const size_t off = head + t0 * V * W;
+                Inputs<T, K> ic;
+                for (int k = 0; k < K; k++) ic.p[k] = in.p[k] + off;
+                hipLaunchKernelGGL(kernel, dim3((unsigned) nt), dim3(threads), 0, s, out + off, ic, nv,
+                                   (size_t) 0, (size_t) 0, 0);
+            }
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
     if constexpr (K >= 2 && K <= kCombineLdsMaxK) {
         constexpr int UL = K == 2 ? OSGPU_COMBINE_LDS_U2 : kCombineLdsU;
-        size_t blocks = (nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL);
-        if (blocks == 0) blocks = 1;
-        if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((combine_lds_kernel<T, OP, K, UL>), dim3((unsigned) blocks),
-                           dim3(64 * K), 0, s, out, in, nvec, head, tail_start, nedge);
-        return hipGetLastError();
+        return launch((size_t) 64 * UL, 64 * K, combine_lds_kernel<T, OP, K, UL>);
     }
-    size_t per_block = (size_t) kBlock * U;
-    size_t blocks = (nvec + per_block - 1) / per_block;
-    if (blocks == 0) blocks = 1;
-    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((combine_vec_kernel<T, OP, K>), dim3((unsigned) blocks),
-                       dim3(kBlock), 0, s, out, in, nvec, head, tail_start, nedge);
-    return hipGetLastError();
+    return launch((size_t) kBlock * U, kBlock, combine_vec_kernel<T, OP, K>);
 }
 
 constexpr int kMaxK = 8;

@@ -29,6 +29,17 @@ hipError_t launch_combine(int type, int op, void *out, const void *const *srcs, 
 // remote: some member's arrays live in another GPU's HBM (xGMI) -- the team
 // kernel then takes the shapes last measured across GPUs (team.hip TeamShape)
 constexpr int kMaxTeam = 8;
+
+// Threads per launch of the one-tile-per-workgroup kernels (combine_lds,
+// combine_vec, team_lds, team_vec): a grid's thread count must stay below
+// 2^32 (HIP refuses larger grids: an 8-member team call of 1 Gi doubles,
+// config 4's shape, needs 2^32 threads in the LDS form), so a larger call
+// runs as several launches over consecutive runs of tiles.
+constexpr size_t kMaxLaunchThreads = (size_t) 1 << 31;
+// the limit in force: kMaxLaunchThreads, or a smaller one a test set
+// (osgpu_test_max_launch_threads) to run the multi-launch path at small sizes
+size_t max_launch_threads();
+void set_max_launch_threads(size_t n);
 hipError_t launch_team(int type, int op, int P, void *const *dsts, const void *const *srcs,
                        size_t n, hipStream_t s, bool remote = false);
 hipError_t launch_team_longdouble(int op, int P, void *const *dsts, const void *const *srcs,

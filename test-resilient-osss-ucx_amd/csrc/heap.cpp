@@ -1099,6 +1099,24 @@ extern "C" int osgpu_preflight(void *heap_base, int PE_start, int logPE_stride, 
 // Not in the public header (tests/support/osgpu_test_hooks.h) and refused
 // unless the process runs with OSGPU_TEST_HOOKS=1: a production caller can
 // never redirect preflight writes by accident.
+// Launch-size limit for the one-tile-per-workgroup kernels
+// (combine.hpp kMaxLaunchThreads): a smaller limit runs their multi-launch
+// path at small sizes.  n <= 0 restores the default.  Test hooks only.
+extern "C" int osgpu_test_max_launch_threads(long long n)
+{
+    const char *on = getenv("OSGPU_TEST_HOOKS");
+    if (!on || strcmp(on, "1")) {
+        set_err("osgpu_test_max_launch_threads: test hooks are off (OSGPU_TEST_HOOKS=1 enables them)");
+        return OSGPU_EINVAL;
+    }
+    const size_t lim = n <= 0 || (size_t) n > osgpu::kMaxLaunchThreads ? osgpu::kMaxLaunchThreads
+                                                                       : (size_t) n;
+    osgpu::set_max_launch_threads(lim);
+    if (lim != osgpu::kMaxLaunchThreads)
+        fprintf(stderr, "[osgpu] test hook: at most %zu threads per kernel launch\n", lim);
+    return OSGPU_OK;
+}
+
 extern "C" int osgpu_test_preflight_fault(int pe, int peer)
 {
     const char *on = getenv("OSGPU_TEST_HOOKS");

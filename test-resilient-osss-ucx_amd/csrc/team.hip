@@ -481,19 +481,45 @@ static hipError_t team_launch_p(void *const *dsts, const void *const *srcs, size
     const size_t tail_start = head + nvec * W;
     // the unaligned head and the tail: member 0's first workgroup
     const int nedge = tl.k == 0 ? (int) (head + (n - tail_start)) : 0;
+    // tiles of V vectors, this member's every tl.m-th one, one per workgroup
+    // of `threads`; at most max_launch_threads() per launch (combine.hpp):
+    // runs of tiles that are whole multiples of tl.m, so tile t of a run is
+    // still this member's when t % tl.m == tl.k; the first launch takes the
+    // edges, the others shifted pointers
+    auto launch = [&](size_t V, unsigned threads, auto kernel) -> hipError_t {
+        size_t tiles = (nvec + V - 1) / V;
+        if (tiles == 0) tiles = 1;
+        const size_t lim = max_launch_threads() / threads;
+        const size_t run = (lim ? lim : 1) * tl.m;
+        for (size_t t0 = 0; t0 < tiles; t0 += run) {
+            const size_t nt = tiles - t0 < run ? tiles - t0 : run;
+            const size_t nv = nvec - t0 * V < nt * V ? nvec - t0 * V : nt * V;
+            const size_t blocks = tl.blocks(nt);
+            if (t0 == 0) {
+                hipLaunchKernelGGL(kernel, dim3((unsigned) blocks), dim3(threads), 0, s, a, nv, head,
+                                   tail_start, nedge, tl.m, tl.k);
+            } else {
+                const size_t off = head + t0 * V * W;
+                TeamPtrs<T, P> c;
+                for (int p = 0; p < P; p++) {
+                    c.src[p] = a.src[p] + off;
+                    c.dst[p] = a.dst[p] + off;
+                }
+                hipLaunchKernelGGL(kernel, dim3((unsigned) blocks), dim3(threads), 0, s, c, nv,
+                                   (size_t) 0, (size_t) 0, 0, tl.m, tl.k);
+            }
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
     if constexpr (S::kLds) {
         constexpr int UL = S::kLdsU;
-        const size_t blocks = tl.blocks((nvec + (size_t) 64 * UL - 1) / ((size_t) 64 * UL));
-        hipLaunchKernelGGL((team_lds_kernel<T, OP, P, ORDERED, UL>), dim3((unsigned) blocks),
-                           dim3(64 * P), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
+        return launch((size_t) 64 * UL, 64 * P, team_lds_kernel<T, OP, P, ORDERED, UL>);
     } else {  // (not instantiated where the LDS form is used)
-        constexpr int U = S::U;
-        const size_t blocks =
-            tl.blocks((nvec + (size_t) kTeamBlock * U - 1) / ((size_t) kTeamBlock * U));
-        hipLaunchKernelGGL((team_vec_kernel<T, OP, P, ORDERED, REMOTE>), dim3((unsigned) blocks),
-                           dim3(kTeamBlock), 0, s, a, nvec, head, tail_start, nedge, tl.m, tl.k);
+        return launch((size_t) kTeamBlock * S::U, kTeamBlock,
+                      team_vec_kernel<T, OP, P, ORDERED, REMOTE>);
     }
-    return hipGetLastError();
 }
 
 // the remote shape only where it differs from the local one

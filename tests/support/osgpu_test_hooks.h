@@ -11,6 +11,11 @@ extern "C" {
  * legs must report.  (-1, -1) clears it; it is logged on stderr while set. */
 int osgpu_test_preflight_fault(int pe, int peer);
 
+/* At most n threads per launch of the one-tile-per-workgroup kernels
+ * (combine.hpp kMaxLaunchThreads, 2^31): a smaller n runs their multi-launch
+ * path at small sizes.  n <= 0 restores the default; logged on stderr. */
+int osgpu_test_max_launch_threads(long long n);
+
 #ifdef __cplusplus
 }
 #endif

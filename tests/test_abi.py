@@ -281,6 +281,10 @@ def test_test_hook_refused_in_production(lib, monkeypatch):
     lib.osgpu_test_preflight_fault.argtypes = [ctypes.c_int, ctypes.c_int]
     assert lib.osgpu_test_preflight_fault(0, 1) != 0
     assert b"test hooks are off" in lib.osgpu_last_error()
+    assert "osgpu_test_max_launch_threads" not in hdr
+    lib.osgpu_test_max_launch_threads.argtypes = [ctypes.c_longlong]
+    assert lib.osgpu_test_max_launch_threads(2048) != 0
+    assert b"test hooks are off" in lib.osgpu_last_error()
 
 
 def test_product_never_references_the_oracle():

@@ -626,3 +626,76 @@ def test_longdouble_same_sign_sums(torch_cuda, P, sign):
         for q in range(P):
             got = outs[q].cpu().numpy().reshape(-1, 16)[:, :10].reshape(-1)
             assert np.array_equal(got, O.value_bytes(want[q]).reshape(-1)), (P, sign, spoil, q)
+
+
+@pytest.fixture
+def small_launches(monkeypatch):
+    """At most 2048 threads per launch for the test (osgpu_test_max_launch_
+    threads, a test hook): every combine and team call of more than a few
+    tiles takes the multi-launch path that calls of 2^31+ threads take (an
+    8-member team call of 1 Gi doubles), at small sizes; restored after."""
+    monkeypatch.setenv("OSGPU_TEST_HOOKS", "1")
+    L = osgpu.load()
+    L.osgpu_test_max_launch_threads.argtypes = [ctypes.c_longlong]
+    assert L.osgpu_test_max_launch_threads(2048) == 0, L.osgpu_last_error()
+    yield
+    assert L.osgpu_test_max_launch_threads(0) == 0
+
+
+@pytest.mark.parametrize("t", ["short", "float", "double", "complexd"])
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+def test_combine_multi_launch(torch_cuda, small_launches, t, k):
+    """The combine kernels over many launches (combine.hip launch_k: the
+    first launch takes the unaligned head and the tail, the others run on
+    shifted pointers): ragged n, 16-byte phases, every element bit-exact."""
+    torch = torch_cuda
+    s = np.dtype(O.NP_DTYPE[t]).itemsize
+    for n in (4099, 100_003):
+        for shift in (0, 1):
+            if s >= 16 and shift:
+                continue
+            ins = [O.gen_input(t, n, 3000 + 7 * j + n, "edge") for j in range(k)]
+            want = ins[0]
+            for x in ins[1:]:
+                want = O.op_elementwise(t, "sum", want, x)
+            bufs = [_dev(torch, np.concatenate([O.gen_input(t, shift, 5, "mixed"), x])) for x in ins]
+            out = torch.zeros((n + shift) * s, dtype=torch.uint8, device="cuda:0")
+            osgpu.combine(t, "sum", out.data_ptr() + shift * s,
+                          [b.data_ptr() + shift * s for b in bufs], n, _stream(torch))
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()[shift * s:]
+            bad = np.nonzero(got.reshape(-1) != O.value_bytes(want).reshape(-1))[0]
+            assert bad.size == 0, (t, k, n, shift, bad[:8] // s)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("t,op", [("double", "sum"), ("int", "xor"), ("float", "max"),
+                                  ("complexf", "prod"), ("short", "min")])
+def test_team_multi_launch(torch_cuda, small_launches, P, t, op):
+    """The team kernels (LDS form at 2-4 and, real types, 8 members; register
+    form otherwise) over many launches (team.hip team_launch_p): ragged n,
+    one 16-byte phase for every array, every member's result bit-exact
+    against its own fold order."""
+    torch = torch_cuda
+    s = np.dtype(O.NP_DTYPE[t]).itemsize
+    L = osgpu.load()
+    for n in (5_001, 100_003):
+        for shift in (0, 1):
+            if s >= 16 and shift:
+                continue
+            srcs = [O.gen_input(t, n, 4000 + 11 * p + n, "edge") for p in range(P)]
+            want = O.to_all(t, op, srcs)
+            pad = O.gen_input(t, shift, 5, "mixed")
+            ins = [_dev(torch, np.concatenate([pad, x])) for x in srcs]
+            outs = [torch.zeros((n + shift) * s, dtype=torch.uint8, device="cuda:0")
+                    for _ in range(P)]
+            S = (ctypes.c_void_p * P)(*[x.data_ptr() + shift * s for x in ins])
+            D = (ctypes.c_void_p * P)(*[y.data_ptr() + shift * s for y in outs])
+            torch.cuda.synchronize()
+            assert L.osgpu_team_combine(osgpu.TYPES.index(t), osgpu.OPS.index(op), P, D, S, n,
+                                        None) == 0, L.osgpu_last_error()
+            torch.cuda.synchronize()
+            for q in range(P):
+                got = outs[q].cpu().numpy()[shift * s:]
+                bad = np.nonzero(got.reshape(-1) != O.value_bytes(want[q]).reshape(-1))[0]
+                assert bad.size == 0, (t, op, P, n, shift, q, bad[:8] // s)
