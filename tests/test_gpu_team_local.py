@@ -28,6 +28,12 @@ sys.path[:0] = [os.path.join(root, "tests"), os.path.join(root, "oracle"),
 import torch
 assert torch.cuda.is_available()
 import test_gpu_parity as G
+if os.environ.get("TEST_MAX_LAUNCH_THREADS"):  # the multi-launch path (a test hook)
+    import ctypes
+    import osgpu
+    L = osgpu.load()
+    L.osgpu_test_max_launch_threads.argtypes = [ctypes.c_longlong]
+    assert L.osgpu_test_max_launch_threads(int(os.environ["TEST_MAX_LAUNCH_THREADS"])) == 0
 tm = G.team()
 bad, paths, n = [], {}, 0
 for c in G.CASES:
@@ -43,14 +49,18 @@ print(json.dumps({"cases": n, "nbad": len(bad), "bad": bad[:5], "paths": paths})
 """
 
 
-@pytest.mark.parametrize("mode", ["shards", "tiles", "merge+block"])
+@pytest.mark.parametrize("mode", ["shards", "tiles", "merge+block", "tiles+small"])
 def test_team_local_modes_match_golden(mode):
     # +block: OSGPU_SYNC=block (hipStreamSynchronize) instead of the default
-    # completion word (runtime.cpp stream_wait)
-    local, _, sync = mode.partition("+")
+    # completion word (runtime.cpp stream_wait); +small: at most 2048 threads
+    # per launch (test hook), so the tiles of every member k of m run over
+    # several launches (team.hip team_launch_p: runs of whole multiples of m)
+    local, _, extra = mode.partition("+")
     env = dict(os.environ, OSGPU_TEAM_LOCAL=local)
-    if sync:
-        env["OSGPU_SYNC"] = sync
+    if extra == "block":
+        env["OSGPU_SYNC"] = extra
+    elif extra == "small":
+        env.update(OSGPU_TEST_HOOKS="1", TEST_MAX_LAUNCH_THREADS="2048")
     r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], env=env, capture_output=True,
                        text=True, timeout=280)
     assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
