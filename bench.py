@@ -48,9 +48,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # member counts that kernel serves (OSGPU_TEAM_LDS_MIN_P, OSGPU_TEAM_LDS_MAX_P)
 TEAM_LDS_U = 1
 TEAM_LDS_P = (2, 4)
-# ... and the LDS form also at 8 members for real types other than FP
-# max/min (double sum among them), when no member is remote (TeamShape kLds)
-TEAM_LDS_EXTRA_P = (8,)
+# ... and the LDS form also at 5, 6 and 8 members for real types other than
+# FP max/min (double sum among them), when no member is remote (TeamShape kLds)
+TEAM_LDS_EXTRA_P = (5, 6, 8)
 
 
 def team_lds(P, remote=False):
@@ -846,7 +846,7 @@ def team_kernel_rate(L, torch, n, reps, P=2, arrays=None, layout="alloc", canary
     can_after = canary() if canary is not None else None
     B = 2 * P * n * 8
     # the form team.hip launches for double sum (TeamShape): the LDS-staged
-    # kernel (U = TEAM_LDS_U) at 2 to 4 and at 8 members, the register kernel
+    # kernel (U = TEAM_LDS_U) at 2 to 6 and at 8 members, the register kernel
     # otherwise
     lds = team_lds(P)
     kern = (f"team_lds_kernel<double, 0, {P}, true, {TEAM_LDS_U}" if lds    # (PMC files' key)

@@ -98,10 +98,9 @@ constexpr int kTeamU4 = 4;
 // prod 1.09x at 4, complex double prod 1.05-1.09x), lifting the 4-member
 // kernel from 0.963 to 1.021 of the same-mix copy
 // (profiles/r06_team_lds_u1_ab.jsonl: 1.04x / 1.00x / 1.09x for double
-// sum).  The same form at 5-7 members is mixed -- 1.07x at 5 and 6 for
-// double sum, 0.89x at 7 -- so 5-7 keep the register form; at 8 it wins for
-// real types other than FP max/min (TeamShape kLds below) and loses for
-// complex ones (0.72x for complex double prod).  (Round 5 had U = 2 over U = 4, 1.02-1.04x,
+// sum).  Above 4 members it wins at 5, 6 and 8 for real types other than
+// FP max/min (TeamShape kLds below) and loses at 7 and for complex types
+// (0.72x for complex double prod at 8): those keep the register form.  (Round 5 had U = 2 over U = 4, 1.02-1.04x,
 // r05_team_p34_ab.jsonl; LDS-DMA staging at 4 members 0.967-0.998x,
 // r06_team_p4_ab.jsonl.)  The combine keeps U = 2: U = 1 there ran 0.966x.
 #ifndef OSGPU_TEAM_LDS_U
@@ -121,18 +120,19 @@ struct TeamShape {
                              : (kHeavy ? kTeamGH : ((kComplex || REMOTE) ? kTeamG8 : OSGPU_TEAM_G8R));
     static constexpr bool kPipe = P > 4 && U / G > 1 && std::is_integral<T>::value;
     static constexpr bool kPerOutput = P > 4;
-    // the LDS form also at 8 members for real types other than FP max/min:
-    // in one process on the same allocations every (type, op) tried ran
-    // faster (double sum 1.012x, float sum 1.043x, int sum 1.085x, long xor
-    // 1.068x, short min 1.060x, float prod 1.042x, double prod 1.110x, int
-    // max 1.090x, long sum 1.042x median of 5, min 0.979x;
-    // profiles/r06_team_lds8_ab.jsonl); complex types and FP max/min lost
-    // there (0.72-0.98x, profiles/r06_team_lds_p58_ab.jsonl), as did 5-7
-    // members (mixed).
+    // the LDS form also at 5, 6 and 8 members for real types other than FP
+    // max/min: in one process on the same allocations, 9 (type, op) cases x
+    // 5 allocations, at 8 members every case ran faster (double sum 1.012x,
+    // float sum 1.043x, int sum 1.085x, long xor 1.068x, short min 1.060x,
+    // float prod 1.042x, double prod 1.110x, int max 1.090x, long sum
+    // 1.042x; profiles/r06_team_lds8_ab.jsonl), at 5 and 6 members 1.058x
+    // overall (cases 0.989-1.110x; r06_team_lds56_ab.jsonl); complex types
+    // and FP max/min lost (0.72-0.98x, r06_team_lds_p58_ab.jsonl), and so
+    // did every case at 7 members (7-wave workgroups, 0.78-0.99x).
     static constexpr bool kFpMinMax = std::is_floating_point<T>::value && (OP == OP_MAX || OP == OP_MIN);
     static constexpr bool kLds = REMOTE ? (P >= 3 && P <= 4)
                                         : ((P >= OSGPU_TEAM_LDS_MIN_P && P <= OSGPU_TEAM_LDS_MAX_P) ||
-                                           (P == 8 && !kComplex && !kFpMinMax));
+                                           ((P == 5 || P == 6 || P == 8) && !kComplex && !kFpMinMax));
     static constexpr int kLdsU = OSGPU_TEAM_LDS_U;
     // the rounds g = 0, G, 2G, ... must tile [0, U) exactly, or the last
     // round reads and writes past the tile (and past nvec)

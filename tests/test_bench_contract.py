@@ -130,7 +130,8 @@ def test_bench_names_the_shipped_lds_tile():
     hi = re.search(r"#define OSGPU_TEAM_LDS_MAX_P (\d+)", src)
     assert (int(lo.group(1)), int(hi.group(1))) == bench.TEAM_LDS_P
     # the 8-member LDS rule for real types (TeamShape kLds) and bench's mirror
-    assert "(P == 8 && !kComplex && !kFpMinMax)" in src and bench.TEAM_LDS_EXTRA_P == (8,)
+    assert ("((P == 5 || P == 6 || P == 8) && !kComplex && !kFpMinMax)" in src
+            and bench.TEAM_LDS_EXTRA_P == (5, 6, 8))
     assert bench.team_lds(8) and not bench.team_lds(8, remote=True) and not bench.team_lds(7)
     comb = open(os.path.join(ROOT, "test-resilient-osss-ucx_amd", "csrc", "combine.hip")).read()
     kmax = re.search(r"constexpr int kCombineLdsMaxK = (\d+);", comb)
